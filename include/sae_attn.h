@@ -1,0 +1,155 @@
+/*
+ * sae_attn.h -- C ABI of the MI355X (gfx950) multi-head self-attention hot path.
+ *
+ * This is the drop-in boundary of the build: every entry point takes plain device
+ * pointers, sizes and a HIP stream (as void*), never a framework type.  It replaces the
+ * XLA-lowered einsum / softmax chains of the reference's Flax attention modules
+ * (cfoster0/self-attention-experiments-vision):
+ *
+ *   sae_attn_fwd / sae_attn_bwd
+ *       AttentionBlock core, models/layers/attentions/attention.py:39-58
+ *       (q/sqrt(D) :39, QK^T einsum :41-42, softmax :48, AV einsum :57-58) and its JAX
+ *       autodiff backward.  Also the core of CvTAttentionBlock
+ *       (models/layers/attentions/cvt_attention.py:85-104, Nq != Nk), of
+ *       ClassSelfAttentionBlock (models/cait.py:10-15, Nq = 1) and of
+ *       LCSelfAttentionBlock (models/ceit.py:11-16, Nq = 1).
+ *   SAE_FLAG_RELPOS (bias_h / bias_w in sae_attn_fwd/bwd) + sae_relpos_bias_fwd/bwd
+ *       BoTNet RelativeLogits added to the score tile, models/botnet.py:70-141,191-192.
+ *   sae_th_attn_fwd / sae_th_attn_bwd
+ *       talking-heads attention, attention.py:44-52 + talking_heads.py:9-14.
+ *   sae_rotary
+ *       rotary position embedding, models/layers/position_embed.py:8-20 (README to-do).
+ *
+ * Conventions
+ *   - Activations are token-major [B, N, H, D] (the reference einsum layout), addressed by
+ *     element strides (batch, token, head); the head_dim stride is 1.
+ *   - Scores are scale * <q, k> (+ bias); the reference's scale is 1/sqrt(head_ch).
+ *   - lse is float32 [B, H, Nq], the natural-log log-sum-exp of each score row.
+ *   - dtype is SAE_DTYPE_BF16 (compute: bf16 MFMA, fp32 accumulate / softmax) or
+ *     SAE_DTYPE_F32 (exact fp32 MFMA).
+ *   - All buffers are caller-owned; nothing is allocated or retained; every launch is
+ *     ordered on `stream`; no host synchronisation (graph-capturable); re-entrant.
+ *   - Return 0 on success, a negative SAE_E* code otherwise; sae_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ */
+#ifndef SAE_ATTN_H
+#define SAE_ATTN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAE_ABI_VERSION 1
+
+enum {
+  SAE_OK = 0,
+  SAE_EINVAL = -1,        /* descriptor / argument validation failed */
+  SAE_EUNSUPPORTED = -2,  /* valid but outside the implemented envelope (e.g. D > 128) */
+  SAE_EHIP = -3           /* a HIP runtime call failed */
+};
+
+enum { SAE_DTYPE_F32 = 0, SAE_DTYPE_BF16 = 1 };
+
+enum { SAE_FLAG_RELPOS = 1 };
+
+typedef struct sae_attn_desc {
+  int32_t batch, heads, seq_q, seq_k, head_dim;
+  int32_t dtype;          /* SAE_DTYPE_* of q, k, v, o, dout, dq, dk, dv */
+  int32_t flags;          /* SAE_FLAG_* */
+  float scale;            /* score = scale * <q, k> + bias */
+  /* element strides (batch, token, head); head_dim stride must be 1 */
+  int64_t q_stride[3], k_stride[3], v_stride[3], o_stride[3];
+  /* backward only */
+  int64_t do_stride[3], dq_stride[3], dk_stride[3], dv_stride[3];
+  /* SAE_FLAG_RELPOS: keys form a rel_h x rel_w grid (seq_k == rel_h * rel_w) and
+     bias_h [B,H,Nq,rel_h], bias_w [B,H,Nq,rel_w] (fp32) are added to the scores:
+     score[q, k] += bias_h[q, k / rel_w] + bias_w[q, k % rel_w]. */
+  int32_t rel_h, rel_w;
+} sae_attn_desc;
+
+/* Fill `desc` for contiguous [B, N, H, D] tensors (all eight stride triples). */
+void sae_attn_desc_init(sae_attn_desc* desc, int32_t batch, int32_t heads, int32_t seq_q,
+                        int32_t seq_k, int32_t head_dim, int32_t dtype, float scale);
+
+/* Forward: o = softmax(scale q k^T + bias) v, lse = logsumexp rows.
+   bias_h / bias_w may be NULL unless SAE_FLAG_RELPOS.  lse may be NULL (inference). */
+int sae_attn_fwd(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                 const void* v, const float* bias_h, const float* bias_w, void* o,
+                 float* lse);
+
+/* Bytes of device workspace sae_attn_bwd needs (float32 delta = rowsum(dout * o)). */
+size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* desc);
+
+/* Backward: writes dq, dk, dv (and dbias_h / dbias_w if SAE_FLAG_RELPOS: the score
+   gradient summed over key rows / key columns).  Deterministic: no atomics to HBM. */
+int sae_attn_bwd(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                 const void* v, const void* o, const float* lse, const void* dout,
+                 const float* bias_h, const float* bias_w, void* dq, void* dk, void* dv,
+                 float* dbias_h, float* dbias_w, void* workspace);
+
+/* BoTNet relative logits (botnet.py:70-141) in index-map form, qhat = scaled query
+   [B, N = Hs*Ws, H, D] (dtype), emb_h [2Hs-1, D], emb_w [2Ws-1, D] fp32:
+     bias_h[b,h,n,p] = <qhat[b,n,h], emb_h[p - n/Ws + Hs - 1]>
+     bias_w[b,h,n,c] = <qhat[b,n,h], emb_w[c - n%Ws + Ws - 1]>                        */
+int sae_relpos_bias_fwd(void* stream, int32_t batch, int32_t heads, int32_t rel_h,
+                        int32_t rel_w, int32_t head_dim, int32_t dtype, const void* qhat,
+                        const int64_t qhat_stride[3], const float* emb_h,
+                        const float* emb_w, float* bias_h, float* bias_w);
+
+size_t sae_relpos_bias_bwd_workspace_bytes(int32_t batch, int32_t rel_h, int32_t rel_w,
+                                           int32_t head_dim);
+
+/* Backward of sae_relpos_bias_fwd.  dqhat_out = dqhat_in + d(bias)/d(qhat)
+   (dqhat_in may equal dqhat_out, or be NULL for zero), demb_h / demb_w overwritten. */
+int sae_relpos_bias_bwd(void* stream, int32_t batch, int32_t heads, int32_t rel_h,
+                        int32_t rel_w, int32_t head_dim, int32_t dtype, const void* qhat,
+                        const int64_t qhat_stride[3], const float* emb_h,
+                        const float* emb_w, const float* dbias_h, const float* dbias_w,
+                        const void* dqhat_in, void* dqhat_out, const int64_t dq_stride[3],
+                        float* demb_h, float* demb_w, void* workspace);
+
+/* Rotary embedding (position_embed.py:8-20, GPT-J interleaved pairs) on x [B,N,H,D]:
+     y[2i]   = x[2i] cos[n,i] - x[2i+1] sin[n,i]
+     y[2i+1] = x[2i+1] cos[n,i] + x[2i] sin[n,i]
+   sin/cos are fp32 [N, D/2] tables.  inverse != 0 rotates by -theta (the backward).
+   y may alias x. */
+int sae_rotary(void* stream, int32_t batch, int32_t seq, int32_t heads, int32_t head_dim,
+               int32_t dtype, const void* x, const int64_t x_stride[3], void* y,
+               const int64_t y_stride[3], const float* sin_tab, const float* cos_tab,
+               int32_t inverse);
+
+/* Talking-heads attention (attention.py:41-58 with talking_heads=True):
+     S = scale q k^T ; S1[i] = sum_h th1[h,i] S[h] ; P = softmax(S1) ;
+     P2[i] = sum_h th2[h,i] P[h] ; o = P2 v
+   th1/th2 are fp32 [H, H] ([h_in, h_out], talking_heads.py:13).  One workgroup holds one
+   query (or key) block for all heads, so heads <= SAE_TH_MAX_HEADS and head_dim <=
+   SAE_TH_MAX_HEAD_DIM (every CaiT config of models/create_model.py:79-150 fits).
+   lse: fp32 [B, H, Nq] log-sum-exp of the mixed logits S1 (for the backward). */
+#define SAE_TH_MAX_HEADS 8
+#define SAE_TH_MAX_HEAD_DIM 64
+int sae_th_attn_fwd(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                    const void* v, const float* th1, const float* th2, void* o, float* lse);
+
+size_t sae_th_attn_bwd_workspace_bytes(const sae_attn_desc* desc);
+
+/* Backward of sae_th_attn_fwd: dq, dk, dv and the transform gradients dth1, dth2
+   (fp32 [H, H], overwritten; reduced deterministically through the workspace). */
+int sae_th_attn_bwd(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                    const void* v, const float* th1, const float* th2, const float* lse,
+                    const void* dout, void* dq, void* dk, void* dv, float* dth1,
+                    float* dth2, void* workspace);
+
+/* Thread-local message describing the last failure on this thread ("" if none). */
+const char* sae_last_error(void);
+
+/* ABI version (SAE_ABI_VERSION) and a build string. */
+int32_t sae_abi_version(void);
+const char* sae_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAE_ATTN_H */

@@ -1,0 +1,476 @@
+// attn_kernels.h -- fused flash-style attention forward / backward for gfx950.
+//
+// Replaces the XLA chain of models/layers/attentions/attention.py:39-58 (q/sqrt(D), QK^T
+// einsum, softmax, AV einsum) and its autodiff backward.  Layout is the reference's
+// token-major [B, N, H, D]; the scores never touch HBM.
+//
+// Forward (attn_fwd): one 256-thread workgroup = 4 waves = 128 query rows of one (b, h);
+// each wave owns 32 query rows with the query on the MFMA lane ("swapped" QK^T: S^T = K Q^T),
+// so the online-softmax state (m, l) and the O^T rescale are per-lane scalars.  K/V tiles of
+// 64 keys are staged global -> registers -> LDS (loads for tile t+1 in flight during tile t);
+// P^T feeds O^T = V^T P^T straight from the accumulator registers, V^T read with
+// ds_read_b64_tr_b16.
+//
+// Backward = delta pre-pass + two deterministic passes (no HBM atomics):
+//   attn_bwd_dkdv: key on the lane; a workgroup owns 128 keys and sweeps all query tiles,
+//                  S = Q K^T, dP = dO V^T, dV^T += dO^T P, dK^T += Q^T dS.
+//   attn_bwd_dq  : query on the lane; S^T, dP^T recomputed, dQ^T += K^T dS^T (+ the BoTNet
+//                  relative-logit gradient reduced in LDS).
+#pragma once
+#include "common.h"
+
+namespace sae {
+
+struct AttnArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* o;
+  void* out;        // fwd: o; bwd unused
+  float* lse;       // fwd output / bwd input
+  const void* dout;
+  void* dq;
+  void* dk;
+  void* dv;
+  float* delta;     // bwd workspace [B, H, Nq]
+  const float* bias_h;
+  const float* bias_w;
+  float* dbias_h;
+  float* dbias_w;
+  int B, H, Nq, Nk, D;
+  long long qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
+  float scale;
+  int rel_h, rel_w, rel_magic;
+};
+
+constexpr int kBQ = 128;   // query rows per forward / dq workgroup (4 waves x 32)
+constexpr int kBK = 64;    // keys per staged K/V tile
+constexpr int kBKV = 128;  // keys per dkdv workgroup (4 waves x 32)
+constexpr int kBQT = 64;   // query rows per staged tile in dkdv
+
+template <typename T, int DP, bool REL>
+constexpr int fwd_lds_bytes_static() {
+  return 2 * Img<T, DP>::bytes(kBK);
+}
+
+// ================================================================================ forward
+template <typename T, int DP, bool VEC, bool REL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  using M = MF<T>;
+  using I = Img<T, DP>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ldsK = smem;
+  char* ldsV = smem + I::bytes(kBK);
+  float* ldsB = reinterpret_cast<float*>(smem + 2 * I::bytes(kBK));   // REL: [4][32][RW]
+
+  const int nqb = (a.Nq + kBQ - 1) / kBQ;
+  int bid = blockIdx.x;
+  const int qb = bid % nqb;
+  bid /= nqb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * kBQ + w * 32 + r32;
+
+  const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const T* V = reinterpret_cast<const T*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+
+  constexpr int NS = DP / M::KSTEP;        // k-steps over the head dim
+  constexpr int NP = 32 / M::KSTEP;        // k-steps over a 32-key accumulator
+  constexpr int NT = DP / 32;              // 32-wide head-dim tiles of O^T
+
+  typename M::frag qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) qf[s] = gfrag<T, VEC>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+
+  const int RW = a.rel_h + a.rel_w + 1;
+  if constexpr (REL) {
+    // stage this wave's 32 rows of bias_h | bias_w (pre-multiplied by log2 e)
+    float* wb = ldsB + w * 32 * RW;
+    const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+    for (int i = lane; i < 32 * (RW - 1); i += 64) {
+      const int rr = i / (RW - 1), cc = i % (RW - 1);
+      const int qq = qb * kBQ + w * 32 + rr;
+      float val = 0.f;
+      if (qq < a.Nq)
+        val = cc < a.rel_h ? a.bias_h[(rowoff + qq) * a.rel_h + cc]
+                           : a.bias_w[(rowoff + qq) * a.rel_w + (cc - a.rel_h)];
+      wb[rr * RW + cc] = val * kLog2e;
+    }
+  }
+
+  f32x16 acco[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acco[t] = zero16();
+  float m = -kInf, l = 0.f;
+  const float sl2 = a.scale * kLog2e;
+  const int nkt = (a.Nk + kBK - 1) / kBK;
+
+  Stage<T, DP, kBK, VEC> kst, vst;
+  kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
+  vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    kst.write(ldsK, tid);
+    vst.write(ldsV, tid);
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
+      vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
+    }
+    f32x16 sacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sacc[u] = zero16();
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sacc[u] = M::mma(I::rowfrag(ldsK, 32 * u + r32, s, h), qf[s], sacc[u]);
+    }
+    float mx = -kInf;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * kBK + 32 * u + row_of(r, h);
+        float x = sacc[u][r] * sl2;
+        if constexpr (REL) {
+          const int kk = min(key, a.Nk - 1);
+          const int kx = (kk * a.rel_magic) >> 20;
+          const int ky = kk - kx * a.rel_w;
+          const float* wb = ldsB + (w * 32 + r32) * RW;
+          x += wb[kx] + wb[a.rel_h + ky];
+        }
+        x = key < a.Nk ? x : -kInf;
+        sacc[u][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);
+    const float alpha = ex2(m - mn);
+    m = mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = ex2(sacc[u][r] - mn);
+        sacc[u][r] = p;
+        ls += p;
+      }
+    }
+    l = l * alpha + ls;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acco[t][r] *= alpha;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int s2 = 0; s2 < NP; ++s2) {
+        const typename M::frag pf = acc_frag<T>(sacc[u], s2);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acco[t] = M::mma(I::colfrag(ldsV, 32 * u, s2, 32 * t, lane), pf, acco[t]);
+      }
+    }
+  }
+
+  l += __shfl_xor(l, 32);
+  const float inv = 1.f / l;
+  if (q < a.Nq) {
+    T* O = reinterpret_cast<T*>(a.out) + b * a.os[0] + hh * a.os[2] + (long long)q * a.os[1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4<T, VEC>(O, 32 * t + 8 * g + 4 * h, a.D, acco[t][4 * g] * inv, acco[t][4 * g + 1] * inv,
+                       acco[t][4 * g + 2] * inv, acco[t][4 * g + 3] * inv);
+    if (h == 0 && a.lse) a.lse[((size_t)b * a.H + hh) * a.Nq + q] = (m + lg2(l)) * kLn2;
+  }
+}
+
+// ====================================================================== backward: delta
+// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]  (fp32).  One thread per (b, q, h) row.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
+  const long long n = (long long)a.B * a.Nq * a.H;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int hh = (int)(i % a.H);
+  const long long t = i / a.H;
+  const int q = (int)(t % a.Nq);
+  const int b = (int)(t / a.Nq);
+  const T* O = reinterpret_cast<const T*>(a.o) + b * a.os[0] + (long long)q * a.os[1] + hh * a.os[2];
+  const T* G = reinterpret_cast<const T*>(a.dout) + b * a.dos[0] + (long long)q * a.dos[1] + hh * a.dos[2];
+  float acc = 0.f;
+  for (int d = 0; d < a.D; ++d) acc += (float)O[d] * (float)G[d];
+  a.delta[((size_t)b * a.H + hh) * a.Nq + q] = acc;
+}
+
+// ===================================================================== backward: dK, dV
+template <typename T, int DP, bool VEC, bool REL>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  using M = MF<T>;
+  using I = Img<T, DP>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ldsQ = smem;
+  char* ldsG = smem + I::bytes(kBQT);
+  float* ldsL = reinterpret_cast<float*>(smem + 2 * I::bytes(kBQT));   // lse * log2e  [64]
+  float* ldsD = ldsL + kBQT;                                          // delta        [64]
+  float* ldsB = ldsD + kBQT;                                          // REL: [64][RW]
+
+  const int nkb = (a.Nk + kBKV - 1) / kBKV;
+  int bid = blockIdx.x;
+  const int kb = bid % nkb;
+  bid /= nkb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int key = kb * kBKV + w * 32 + r32;
+
+  const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const T* V = reinterpret_cast<const T*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+  const T* G = reinterpret_cast<const T*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
+  const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+
+  constexpr int NS = DP / M::KSTEP;
+  constexpr int NP = 32 / M::KSTEP;
+  constexpr int NT = DP / 32;
+
+  typename M::frag kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = gfrag<T, VEC>(K, key, a.Nk, a.ks[1], a.D, s, h);
+    vf[s] = gfrag<T, VEC>(V, key, a.Nk, a.vs[1], a.D, s, h);
+  }
+  f32x16 adk[NT], adv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) { adk[t] = zero16(); adv[t] = zero16(); }
+
+  const float sl2 = a.scale * kLog2e;
+  const int RW = a.rel_h + a.rel_w + 1;
+  int kx = 0, ky = 0;
+  if constexpr (REL) {
+    const int kk = min(key, a.Nk - 1);
+    kx = (kk * a.rel_magic) >> 20;
+    ky = kk - kx * a.rel_w;
+  }
+  const int nqt = (a.Nq + kBQT - 1) / kBQT;
+
+  Stage<T, DP, kBQT, VEC> qst, gst;
+  qst.load(Q, 0, a.Nq, a.qs[1], a.D, tid);
+  gst.load(G, 0, a.Nq, a.dos[1], a.D, tid);
+
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    qst.write(ldsQ, tid);
+    gst.write(ldsG, tid);
+    if (tid < kBQT) {
+      const int qq = qt * kBQT + tid;
+      ldsL[tid] = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
+      ldsD[tid] = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+    }
+    if constexpr (REL) {
+      for (int i = tid; i < kBQT * (RW - 1); i += 256) {
+        const int rr = i / (RW - 1), cc = i % (RW - 1);
+        const int qq = qt * kBQT + rr;
+        float val = 0.f;
+        if (qq < a.Nq)
+          val = cc < a.rel_h ? a.bias_h[(rowoff + qq) * a.rel_h + cc]
+                             : a.bias_w[(rowoff + qq) * a.rel_w + (cc - a.rel_h)];
+        ldsB[rr * RW + cc] = val * kLog2e;
+      }
+    }
+    __syncthreads();
+    if (qt + 1 < nqt) {
+      qst.load(Q, (qt + 1) * kBQT, a.Nq, a.qs[1], a.D, tid);
+      gst.load(G, (qt + 1) * kBQT, a.Nq, a.dos[1], a.D, tid);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sp = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sp = M::mma(I::rowfrag(ldsQ, 32 * u + r32, s, h), kf[s], sp);
+        dp = M::mma(I::rowfrag(ldsG, 32 * u + r32, s, h), vf[s], dp);
+      }
+      // sp: S[q = 32u + row_of(r,h)][key = lane]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = 32 * u + row_of(r, h);
+        float x = sp[r] * sl2 - ldsL[ql];
+        if constexpr (REL) x += ldsB[ql * RW + kx] + ldsB[ql * RW + a.rel_h + ky];
+        const float p = ex2(x);
+        sp[r] = p;
+        dp[r] = p * (dp[r] - ldsD[ql]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < NP; ++s2) {
+        const typename M::frag pf = acc_frag<T>(sp, s2);
+        const typename M::frag sf = acc_frag<T>(dp, s2);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          adv[t] = M::mma(I::colfrag(ldsG, 32 * u, s2, 32 * t, lane), pf, adv[t]);
+          adk[t] = M::mma(I::colfrag(ldsQ, 32 * u, s2, 32 * t, lane), sf, adk[t]);
+        }
+      }
+    }
+  }
+
+  if (key < a.Nk) {
+    T* DK = reinterpret_cast<T*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)key * a.dks[1];
+    T* DV = reinterpret_cast<T*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)key * a.dvs[1];
+    const float sc = a.scale;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * t + 8 * g + 4 * h;
+        store4<T, VEC>(DK, d0, a.D, adk[t][4 * g] * sc, adk[t][4 * g + 1] * sc, adk[t][4 * g + 2] * sc,
+                       adk[t][4 * g + 3] * sc);
+        store4<T, VEC>(DV, d0, a.D, adv[t][4 * g], adv[t][4 * g + 1], adv[t][4 * g + 2], adv[t][4 * g + 3]);
+      }
+  }
+}
+
+// ========================================================================= backward: dQ
+template <typename T, int DP, bool VEC, bool REL>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  using M = MF<T>;
+  using I = Img<T, DP>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ldsK = smem;
+  char* ldsV = smem + I::bytes(kBK);
+  float* ldsB = reinterpret_cast<float*>(smem + 2 * I::bytes(kBK));   // REL: bias [4][32][RW]
+  // REL: dbias accumulators [4][32][RW] follow the bias tables
+
+  const int nqb = (a.Nq + kBQ - 1) / kBQ;
+  int bid = blockIdx.x;
+  const int qb = bid % nqb;
+  bid /= nqb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * kBQ + w * 32 + r32;
+
+  const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const T* V = reinterpret_cast<const T*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+  const T* G = reinterpret_cast<const T*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
+  const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+
+  constexpr int NS = DP / M::KSTEP;
+  constexpr int NP = 32 / M::KSTEP;
+  constexpr int NT = DP / 32;
+
+  typename M::frag qf[NS], gf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = gfrag<T, VEC>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    gf[s] = gfrag<T, VEC>(G, q, a.Nq, a.dos[1], a.D, s, h);
+  }
+  const bool qok = q < a.Nq;
+  const float lse2 = qok ? a.lse[rowoff + q] * kLog2e : kInf;
+  const float dlt = qok ? a.delta[rowoff + q] : 0.f;
+
+  const int RW = a.rel_h + a.rel_w + 1;
+  float* wb = ldsB + w * 32 * RW;
+  float* wdb = ldsB + 4 * 32 * RW + w * 32 * RW;
+  if constexpr (REL) {
+    for (int i = lane; i < 32 * RW; i += 64) {
+      const int rr = i / RW, cc = i % RW;
+      const int qq = qb * kBQ + w * 32 + rr;
+      float val = 0.f;
+      if (qq < a.Nq && cc < RW - 1)
+        val = cc < a.rel_h ? a.bias_h[(rowoff + qq) * a.rel_h + cc]
+                           : a.bias_w[(rowoff + qq) * a.rel_w + (cc - a.rel_h)];
+      wb[i] = val * kLog2e;
+      wdb[i] = 0.f;
+    }
+  }
+
+  f32x16 adq[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) adq[t] = zero16();
+  const float sl2 = a.scale * kLog2e;
+  const int nkt = (a.Nk + kBK - 1) / kBK;
+
+  Stage<T, DP, kBK, VEC> kst, vst;
+  kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
+  vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    kst.write(ldsK, tid);
+    vst.write(ldsV, tid);
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
+      vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sp = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sp = M::mma(I::rowfrag(ldsK, 32 * u + r32, s, h), qf[s], sp);
+        dp = M::mma(I::rowfrag(ldsV, 32 * u + r32, s, h), gf[s], dp);
+      }
+      // sp: S^T[key = kt*64 + 32u + row_of(r,h)][q = lane]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * kBK + 32 * u + row_of(r, h);
+        float x = sp[r] * sl2 - lse2;
+        int kx = 0, ky = 0;
+        if constexpr (REL) {
+          const int kk = min(key, a.Nk - 1);
+          kx = (kk * a.rel_magic) >> 20;
+          ky = kk - kx * a.rel_w;
+          x += wb[r32 * RW + kx] + wb[r32 * RW + a.rel_h + ky];
+        }
+        const float p = key < a.Nk ? ex2(x) : 0.f;
+        const float ds = p * (dp[r] - dlt);
+        dp[r] = ds;
+        if constexpr (REL) {
+          if (key < a.Nk) {
+            atomicAdd(&wdb[r32 * RW + kx], ds);
+            atomicAdd(&wdb[r32 * RW + a.rel_h + ky], ds);
+          }
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < NP; ++s2) {
+        const typename M::frag sf = acc_frag<T>(dp, s2);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) adq[t] = M::mma(I::colfrag(ldsK, 32 * u, s2, 32 * t, lane), sf, adq[t]);
+      }
+    }
+  }
+
+  if (qok) {
+    T* DQ = reinterpret_cast<T*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q * a.dqs[1];
+    const float sc = a.scale;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4<T, VEC>(DQ, 32 * t + 8 * g + 4 * h, a.D, adq[t][4 * g] * sc, adq[t][4 * g + 1] * sc,
+                       adq[t][4 * g + 2] * sc, adq[t][4 * g + 3] * sc);
+  }
+  if constexpr (REL) {
+    __syncthreads();   // LDS atomics of both lane halves complete (wave-local region, but be safe)
+    for (int i = lane; i < 32 * (RW - 1); i += 64) {
+      const int rr = i / (RW - 1), cc = i % (RW - 1);
+      const int qq = qb * kBQ + w * 32 + rr;
+      if (qq >= a.Nq) continue;
+      const float val = wdb[rr * RW + cc];
+      if (cc < a.rel_h) a.dbias_h[(rowoff + qq) * a.rel_h + cc] = val;
+      else a.dbias_w[(rowoff + qq) * a.rel_w + (cc - a.rel_h)] = val;
+    }
+  }
+}
+
+}  // namespace sae

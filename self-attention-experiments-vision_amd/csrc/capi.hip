@@ -1,0 +1,521 @@
+// capi.hip -- the C ABI (include/sae_attn.h): descriptor validation, template dispatch and
+// stream-ordered launches.  No allocation, no host synchronisation, no global mutable state
+// besides the thread-local error string.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+#include <initializer_list>
+#include <string>
+
+#include "../../include/sae_attn.h"
+#include "attn_kernels.h"
+#include "th_kernels.h"
+#include "variants.h"
+
+using namespace sae;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int ok() {
+  g_err.clear();
+  return SAE_OK;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SAE_EHIP, "%s: launch failed: %s", what, hipGetErrorString(e));
+  return ok();
+}
+
+int elem_size(int dtype) { return dtype == SAE_DTYPE_BF16 ? 2 : 4; }
+
+bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
+
+int pick_dp(int D) { return D <= 32 ? 32 : (D <= 64 ? 64 : (D <= 128 ? 128 : 0)); }
+
+int validate(const sae_attn_desc* d, bool bwd) {
+  if (!d) return fail(SAE_EINVAL, "desc is NULL");
+  if (d->batch < 1 || d->heads < 1 || d->seq_q < 1 || d->seq_k < 1 || d->head_dim < 1)
+    return fail(SAE_EINVAL, "batch/heads/seq_q/seq_k/head_dim must be >= 1 (got %d/%d/%d/%d/%d)", d->batch,
+                d->heads, d->seq_q, d->seq_k, d->head_dim);
+  if (d->dtype != SAE_DTYPE_BF16 && d->dtype != SAE_DTYPE_F32)
+    return fail(SAE_EINVAL, "dtype %d is not SAE_DTYPE_F32 or SAE_DTYPE_BF16", d->dtype);
+  if (!pick_dp(d->head_dim)) return fail(SAE_EUNSUPPORTED, "head_dim %d > 128 is not supported", d->head_dim);
+  if ((d->flags & ~SAE_FLAG_RELPOS) != 0) return fail(SAE_EINVAL, "unknown flags 0x%x", d->flags);
+  if (d->flags & SAE_FLAG_RELPOS) {
+    if (d->rel_h < 1 || d->rel_w < 1 || d->rel_h * d->rel_w != d->seq_k)
+      return fail(SAE_EINVAL, "relpos grid %dx%d does not match seq_k %d", d->rel_h, d->rel_w, d->seq_k);
+    if (d->rel_w > 64 || d->rel_h > 64 || d->seq_k > 4096)
+      return fail(SAE_EUNSUPPORTED, "relpos grid %dx%d exceeds 64x64", d->rel_h, d->rel_w);
+  }
+  if (d->seq_q > (1 << 24) || d->seq_k > (1 << 24)) return fail(SAE_EUNSUPPORTED, "sequence too long");
+  (void)bwd;
+  return SAE_OK;
+}
+
+bool strides_vec(const int64_t* s, int epc) { return s[0] % epc == 0 && s[1] % epc == 0 && s[2] % epc == 0; }
+
+void fill_args(AttnArgs& a, const sae_attn_desc* d) {
+  memset(&a, 0, sizeof a);
+  a.B = d->batch;
+  a.H = d->heads;
+  a.Nq = d->seq_q;
+  a.Nk = d->seq_k;
+  a.D = d->head_dim;
+  for (int i = 0; i < 3; ++i) {
+    a.qs[i] = d->q_stride[i];
+    a.ks[i] = d->k_stride[i];
+    a.vs[i] = d->v_stride[i];
+    a.os[i] = d->o_stride[i];
+    a.dos[i] = d->do_stride[i];
+    a.dqs[i] = d->dq_stride[i];
+    a.dks[i] = d->dk_stride[i];
+    a.dvs[i] = d->dv_stride[i];
+  }
+  a.scale = d->scale;
+  if (d->flags & SAE_FLAG_RELPOS) {
+    a.rel_h = d->rel_h;
+    a.rel_w = d->rel_w;
+    a.rel_magic = div_magic(d->rel_w);
+  }
+}
+
+// ---------------------------------------------------------------- template dispatch helpers
+template <template <typename, int, bool, bool> class L, typename... Args>
+int dispatch(int dtype, int dp, bool vec, bool rel, Args&&... args) {
+#define SAE_CASE(T, DPV)                                                            \
+  if (dp == DPV) {                                                                  \
+    if (vec) return rel ? L<T, DPV, true, true>::run(args...) : L<T, DPV, true, false>::run(args...); \
+    return rel ? L<T, DPV, false, true>::run(args...) : L<T, DPV, false, false>::run(args...);        \
+  }
+  if (dtype == SAE_DTYPE_BF16) {
+    SAE_CASE(__bf16, 32) SAE_CASE(__bf16, 64) SAE_CASE(__bf16, 128)
+  } else {
+    SAE_CASE(float, 32) SAE_CASE(float, 64) SAE_CASE(float, 128)
+  }
+#undef SAE_CASE
+  return fail(SAE_EUNSUPPORTED, "no kernel instance for dtype %d dp %d", dtype, dp);
+}
+
+int rel_lds_floats(const AttnArgs& a) { return a.rel_h ? 32 * (a.rel_h + a.rel_w + 1) : 0; }
+
+template <typename T, int DP, bool VEC, bool REL> struct FwdL {
+  static int run(hipStream_t st, const AttnArgs& a) {
+    const int nqb = (a.Nq + kBQ - 1) / kBQ;
+    const long long grid = (long long)nqb * a.H * a.B;
+    if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+    size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 4 * rel_lds_floats(a) * sizeof(float) : 0);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+    return check_launch("attn_fwd");
+  }
+};
+
+template <typename T, int DP, bool VEC, bool REL> struct BwdL {
+  static int run(hipStream_t st, const AttnArgs& a) {
+    {
+      const long long n = (long long)a.B * a.Nq * a.H;
+      hipLaunchKernelGGL((attn_bwd_delta_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+      int rc = check_launch("attn_bwd_delta");
+      if (rc) return rc;
+    }
+    {
+      const int nkb = (a.Nk + kBKV - 1) / kBKV;
+      const long long grid = (long long)nkb * a.H * a.B;
+      size_t lds = 2 * Img<T, DP>::bytes(kBQT) + 2 * kBQT * sizeof(float) +
+                   (REL ? (size_t)kBQT * (a.rel_h + a.rel_w + 1) * sizeof(float) : 0);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+      int rc = check_launch("attn_bwd_dkdv");
+      if (rc) return rc;
+    }
+    {
+      const int nqb = (a.Nq + kBQ - 1) / kBQ;
+      const long long grid = (long long)nqb * a.H * a.B;
+      size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 8 * rel_lds_floats(a) * sizeof(float) : 0);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+      return check_launch("attn_bwd_dq");
+    }
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ talking-heads launchers
+namespace {
+void fill_th(ThArgs& a, const sae_attn_desc* d) {
+  memset(&a, 0, sizeof a);
+  a.B = d->batch;
+  a.H = d->heads;
+  a.Nq = d->seq_q;
+  a.Nk = d->seq_k;
+  a.D = d->head_dim;
+  for (int i = 0; i < 3; ++i) {
+    a.qs[i] = d->q_stride[i];
+    a.ks[i] = d->k_stride[i];
+    a.vs[i] = d->v_stride[i];
+    a.os[i] = d->o_stride[i];
+    a.dos[i] = d->do_stride[i];
+    a.dqs[i] = d->dq_stride[i];
+    a.dks[i] = d->dk_stride[i];
+    a.dvs[i] = d->dv_stride[i];
+  }
+  a.scale = d->scale;
+}
+
+bool th_vec(const sae_attn_desc* d, std::initializer_list<const void*> ptrs, bool bwd) {
+  const int epc = 16 / elem_size(d->dtype);
+  bool v = d->head_dim % epc == 0 && strides_vec(d->q_stride, epc) && strides_vec(d->k_stride, epc) &&
+           strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc);
+  if (bwd)
+    v = v && strides_vec(d->do_stride, epc) && strides_vec(d->dq_stride, epc) && strides_vec(d->dk_stride, epc) &&
+        strides_vec(d->dv_stride, epc);
+  for (const void* p : ptrs) v = v && aligned16(p);
+  return v;
+}
+
+template <typename T, int DP, bool VEC> int th_fwd_run(hipStream_t st, const ThArgs& a) {
+  const int nqb = (a.Nq + 31) / 32;
+  size_t lds = kTabBytes + 2 * (size_t)a.H * 4096 + (sizeof(T) == 2 ? (size_t)a.H * Img<T, DP>::bytes(32) : 0);
+  hipLaunchKernelGGL((th_fwd_kernel<T, DP, VEC>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  return hipGetLastError() != hipSuccess;
+}
+
+template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a) {
+  const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32;
+  a.nblk = nqb * a.B;
+  size_t lds_q = kTabBytes + 2 * (size_t)a.H * 4096 + (size_t)a.H * 2 * a.H * 64 * sizeof(float) +
+                 (sizeof(T) == 2 ? (size_t)a.H * Img<T, DP>::bytes(32) : 0);
+  hipLaunchKernelGGL((th_bwd_q_kernel<T, DP, VEC>), dim3(nqb * a.B), dim3(64 * a.H), lds_q, st, a);
+  if (hipGetLastError() != hipSuccess) return 1;
+  size_t lds_kv = kTabBytes + 2 * (size_t)a.H * 4096 + (size_t)a.H * 64 * sizeof(float) +
+                  (sizeof(T) == 2 ? (size_t)a.H * 2 * Img<T, DP>::bytes(32) : 0);
+  hipLaunchKernelGGL((th_bwd_kv_kernel<T, DP, VEC>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
+  if (hipGetLastError() != hipSuccess) return 1;
+  hipLaunchKernelGGL(th_reduce_kernel, dim3((2 * a.H * a.H + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError() != hipSuccess;
+}
+
+}  // namespace
+
+int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
+           const float* th2, void* o, float* lse) {
+  ThArgs a;
+  fill_th(a, d);
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.o = o;
+  a.lse = lse;
+  a.th1 = th1;
+  a.th2 = th2;
+  const bool vec = th_vec(d, {q, k, v, o}, false);
+  hipStream_t st = (hipStream_t)stream;
+  const int dp = pick_dp(d->head_dim);
+#define TH_F(T, DPV) \
+  if (dp == DPV) return vec ? th_fwd_run<T, DPV, true>(st, a) : th_fwd_run<T, DPV, false>(st, a);
+  if (d->dtype == SAE_DTYPE_BF16) {
+    TH_F(__bf16, 32) TH_F(__bf16, 64)
+  } else {
+    TH_F(float, 32) TH_F(float, 64)
+  }
+#undef TH_F
+  return 1;
+}
+
+size_t th_bwd_workspace_bytes(const sae_attn_desc* d) {
+  const size_t delta = (((size_t)d->batch * d->heads * d->seq_q * sizeof(float)) + 255) & ~(size_t)255;
+  const size_t nblk = (size_t)((d->seq_q + 31) / 32) * d->batch;
+  return delta + ((nblk * 2 * d->heads * d->heads * sizeof(float) + 255) & ~(size_t)255);
+}
+
+int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
+           const float* th2, const float* lse, const void* dout, void* dq, void* dk, void* dv, float* dth1,
+           float* dth2, void* workspace) {
+  ThArgs a;
+  fill_th(a, d);
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.lse = const_cast<float*>(lse);
+  a.dout = dout;
+  a.dq = dq;
+  a.dk = dk;
+  a.dv = dv;
+  a.th1 = th1;
+  a.th2 = th2;
+  a.dth1 = dth1;
+  a.dth2 = dth2;
+  a.delta = reinterpret_cast<float*>(workspace);
+  a.part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) +
+                                    ((((size_t)d->batch * d->heads * d->seq_q * sizeof(float)) + 255) & ~(size_t)255));
+  const bool vec = th_vec(d, {q, k, v, dout, dq, dk, dv}, true);
+  hipStream_t st = (hipStream_t)stream;
+  const int dp = pick_dp(d->head_dim);
+#define TH_B(T, DPV) \
+  if (dp == DPV) return vec ? th_bwd_run<T, DPV, true>(st, a) : th_bwd_run<T, DPV, false>(st, a);
+  if (d->dtype == SAE_DTYPE_BF16) {
+    TH_B(__bf16, 32) TH_B(__bf16, 64)
+  } else {
+    TH_B(float, 32) TH_B(float, 64)
+  }
+#undef TH_B
+  return 1;
+}
+
+// ==================================================================================== C ABI
+extern "C" {
+
+void sae_attn_desc_init(sae_attn_desc* d, int32_t batch, int32_t heads, int32_t seq_q, int32_t seq_k,
+                        int32_t head_dim, int32_t dtype, float scale) {
+  memset(d, 0, sizeof *d);
+  d->batch = batch;
+  d->heads = heads;
+  d->seq_q = seq_q;
+  d->seq_k = seq_k;
+  d->head_dim = head_dim;
+  d->dtype = dtype;
+  d->scale = scale;
+  const int64_t hq[3] = {(int64_t)seq_q * heads * head_dim, (int64_t)heads * head_dim, head_dim};
+  const int64_t hk[3] = {(int64_t)seq_k * heads * head_dim, (int64_t)heads * head_dim, head_dim};
+  for (int i = 0; i < 3; ++i) {
+    d->q_stride[i] = d->o_stride[i] = d->do_stride[i] = d->dq_stride[i] = hq[i];
+    d->k_stride[i] = d->v_stride[i] = d->dk_stride[i] = d->dv_stride[i] = hk[i];
+  }
+}
+
+int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                 const float* bias_h, const float* bias_w, void* o, float* lse) {
+  int rc = validate(d, false);
+  if (rc) return rc;
+  if (!q || !k || !v || !o) return fail(SAE_EINVAL, "q/k/v/o must be non-NULL");
+  const bool rel = d->flags & SAE_FLAG_RELPOS;
+  if (rel && (!bias_h || !bias_w)) return fail(SAE_EINVAL, "SAE_FLAG_RELPOS needs bias_h and bias_w");
+  AttnArgs a;
+  fill_args(a, d);
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.out = o;
+  a.lse = lse;
+  a.bias_h = bias_h;
+  a.bias_w = bias_w;
+  const int epc = 16 / elem_size(d->dtype);
+  const bool vec = d->head_dim % epc == 0 && strides_vec(d->q_stride, epc) && strides_vec(d->k_stride, epc) &&
+                   strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) && aligned16(q) &&
+                   aligned16(k) && aligned16(v) && aligned16(o);
+  return dispatch<FwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
+}
+
+size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
+  if (!d) return 0;
+  return (((size_t)d->batch * d->heads * d->seq_q * sizeof(float)) + 255) & ~(size_t)255;
+}
+
+int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                 const void* o, const float* lse, const void* dout, const float* bias_h, const float* bias_w,
+                 void* dq, void* dk, void* dv, float* dbias_h, float* dbias_w, void* workspace) {
+  int rc = validate(d, true);
+  if (rc) return rc;
+  if (!q || !k || !v || !o || !lse || !dout || !dq || !dk || !dv || !workspace)
+    return fail(SAE_EINVAL, "q/k/v/o/lse/dout/dq/dk/dv/workspace must be non-NULL");
+  const bool rel = d->flags & SAE_FLAG_RELPOS;
+  if (rel && (!bias_h || !bias_w || !dbias_h || !dbias_w))
+    return fail(SAE_EINVAL, "SAE_FLAG_RELPOS needs bias_h, bias_w, dbias_h, dbias_w");
+  AttnArgs a;
+  fill_args(a, d);
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.o = o;
+  a.lse = const_cast<float*>(lse);
+  a.dout = dout;
+  a.dq = dq;
+  a.dk = dk;
+  a.dv = dv;
+  a.delta = reinterpret_cast<float*>(workspace);
+  a.bias_h = bias_h;
+  a.bias_w = bias_w;
+  a.dbias_h = dbias_h;
+  a.dbias_w = dbias_w;
+  const int epc = 16 / elem_size(d->dtype);
+  const bool vec = d->head_dim % epc == 0 && strides_vec(d->q_stride, epc) && strides_vec(d->k_stride, epc) &&
+                   strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) &&
+                   strides_vec(d->do_stride, epc) && strides_vec(d->dq_stride, epc) &&
+                   strides_vec(d->dk_stride, epc) && strides_vec(d->dv_stride, epc) && aligned16(q) &&
+                   aligned16(k) && aligned16(v) && aligned16(o) && aligned16(dout) && aligned16(dq) &&
+                   aligned16(dk) && aligned16(dv);
+  return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
+}
+
+// ------------------------------------------------------------------------- relative logits
+static int rel_validate(int B, int H, int Hs, int Ws, int D, int dtype) {
+  if (B < 1 || H < 1 || Hs < 1 || Ws < 1 || D < 1) return fail(SAE_EINVAL, "relpos sizes must be >= 1");
+  if (dtype != SAE_DTYPE_BF16 && dtype != SAE_DTYPE_F32) return fail(SAE_EINVAL, "bad dtype %d", dtype);
+  if (Hs > 64 || Ws > 64) return fail(SAE_EUNSUPPORTED, "relpos grid %dx%d exceeds 64x64", Hs, Ws);
+  return SAE_OK;
+}
+
+int sae_relpos_bias_fwd(void* stream, int32_t B, int32_t H, int32_t Hs, int32_t Ws, int32_t D, int32_t dtype,
+                        const void* qhat, const int64_t qs[3], const float* eh, const float* ew, float* bias_h,
+                        float* bias_w) {
+  int rc = rel_validate(B, H, Hs, Ws, D, dtype);
+  if (rc) return rc;
+  if (!qhat || !qs || !eh || !ew || !bias_h || !bias_w) return fail(SAE_EINVAL, "NULL argument");
+  RelArgs a;
+  memset(&a, 0, sizeof a);
+  a.qhat = qhat;
+  for (int i = 0; i < 3; ++i) a.qs[i] = qs[i];
+  a.eh = eh;
+  a.ew = ew;
+  a.bias_h = bias_h;
+  a.bias_w = bias_w;
+  a.B = B;
+  a.H = H;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.D = D;
+  const long long n = (long long)B * H * Hs * Ws * (Hs + Ws);
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (dtype == SAE_DTYPE_BF16)
+    hipLaunchKernelGGL(relpos_bias_fwd_kernel<__bf16>, g, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(relpos_bias_fwd_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("relpos_bias_fwd");
+}
+
+size_t sae_relpos_bias_bwd_workspace_bytes(int32_t B, int32_t Hs, int32_t Ws, int32_t D) {
+  if (B < 1 || Hs < 1 || Ws < 1 || D < 1) return 0;
+  return (((size_t)B * ((2 * Hs - 1) + (2 * Ws - 1)) * D * sizeof(float)) + 255) & ~(size_t)255;
+}
+
+int sae_relpos_bias_bwd(void* stream, int32_t B, int32_t H, int32_t Hs, int32_t Ws, int32_t D, int32_t dtype,
+                        const void* qhat, const int64_t qs[3], const float* eh, const float* ew,
+                        const float* dbias_h, const float* dbias_w, const void* dq_in, void* dq_out,
+                        const int64_t dqs[3], float* demb_h, float* demb_w, void* workspace) {
+  int rc = rel_validate(B, H, Hs, Ws, D, dtype);
+  if (rc) return rc;
+  if (!qhat || !qs || !eh || !ew || !dbias_h || !dbias_w || !dq_out || !dqs || !demb_h || !demb_w || !workspace)
+    return fail(SAE_EINVAL, "NULL argument");
+  RelArgs a;
+  memset(&a, 0, sizeof a);
+  a.qhat = qhat;
+  for (int i = 0; i < 3; ++i) {
+    a.qs[i] = qs[i];
+    a.dqs[i] = dqs[i];
+  }
+  a.eh = eh;
+  a.ew = ew;
+  a.dbias_h = dbias_h;
+  a.dbias_w = dbias_w;
+  a.dq_in = dq_in;
+  a.dq_out = dq_out;
+  a.demb_h = demb_h;
+  a.demb_w = demb_w;
+  a.part = reinterpret_cast<float*>(workspace);
+  a.B = B;
+  a.H = H;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.D = D;
+  hipStream_t st = (hipStream_t)stream;
+  const long long n1 = (long long)B * Hs * Ws * H * D;
+  const long long n2 = (long long)B * ((2 * Hs - 1) + (2 * Ws - 1)) * D;
+  const int n3 = ((2 * Hs - 1) + (2 * Ws - 1)) * D;
+  if (dtype == SAE_DTYPE_BF16) {
+    hipLaunchKernelGGL(relpos_bias_bwd_dq_kernel<__bf16>, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(relpos_bias_bwd_emb_partial_kernel<__bf16>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0,
+                       st, a);
+  } else {
+    hipLaunchKernelGGL(relpos_bias_bwd_dq_kernel<float>, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(relpos_bias_bwd_emb_partial_kernel<float>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0,
+                       st, a);
+  }
+  hipLaunchKernelGGL(relpos_bias_bwd_emb_reduce_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, st, a);
+  return check_launch("relpos_bias_bwd");
+}
+
+// ---------------------------------------------------------------------------------- rotary
+int sae_rotary(void* stream, int32_t B, int32_t N, int32_t H, int32_t D, int32_t dtype, const void* x,
+               const int64_t xs[3], void* y, const int64_t ys[3], const float* sin_t, const float* cos_t,
+               int32_t inverse) {
+  if (B < 1 || N < 1 || H < 1 || D < 2 || (D & 1)) return fail(SAE_EINVAL, "rotary needs sizes >= 1 and even D");
+  if (dtype != SAE_DTYPE_BF16 && dtype != SAE_DTYPE_F32) return fail(SAE_EINVAL, "bad dtype %d", dtype);
+  if (!x || !xs || !y || !ys || !sin_t || !cos_t) return fail(SAE_EINVAL, "NULL argument");
+  RotArgs a;
+  memset(&a, 0, sizeof a);
+  a.x = x;
+  a.y = y;
+  for (int i = 0; i < 3; ++i) {
+    a.xs[i] = xs[i];
+    a.ys[i] = ys[i];
+  }
+  a.sin_t = sin_t;
+  a.cos_t = cos_t;
+  a.B = B;
+  a.N = N;
+  a.H = H;
+  a.D = D;
+  a.sgn = inverse ? -1.f : 1.f;
+  const long long n = (long long)B * N * H * (D / 2);
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (dtype == SAE_DTYPE_BF16)
+    hipLaunchKernelGGL(rotary_kernel<__bf16>, g, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(rotary_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("rotary");
+}
+
+// --------------------------------------------------------------------------- talking heads
+int sae_th_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                    const float* th1, const float* th2, void* o, float* lse) {
+  int rc = validate(d, false);
+  if (rc) return rc;
+  if (d->flags) return fail(SAE_EINVAL, "talking heads takes no flags");
+  if (!q || !k || !v || !th1 || !th2 || !o || !lse) return fail(SAE_EINVAL, "NULL argument");
+  if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
+    return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
+                SAE_TH_MAX_HEAD_DIM);
+  return th_fwd(stream, d, q, k, v, th1, th2, o, lse) ? fail(SAE_EHIP, "th_fwd launch failed") : check_launch("th_fwd");
+}
+
+size_t sae_th_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
+  if (!d) return 0;
+  return th_bwd_workspace_bytes(d);
+}
+
+int sae_th_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                    const float* th1, const float* th2, const float* lse, const void* dout, void* dq, void* dk,
+                    void* dv, float* dth1, float* dth2, void* workspace) {
+  int rc = validate(d, true);
+  if (rc) return rc;
+  if (d->flags) return fail(SAE_EINVAL, "talking heads takes no flags");
+  if (!q || !k || !v || !th1 || !th2 || !lse || !dout || !dq || !dk || !dv || !dth1 || !dth2 || !workspace)
+    return fail(SAE_EINVAL, "NULL argument");
+  if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
+    return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
+                SAE_TH_MAX_HEAD_DIM);
+  return th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace)
+             ? fail(SAE_EHIP, "th_bwd launch failed")
+             : check_launch("th_bwd");
+}
+
+const char* sae_last_error(void) { return g_err.c_str(); }
+
+int32_t sae_abi_version(void) { return SAE_ABI_VERSION; }
+
+const char* sae_build_info(void) { return "sae_attn gfx950 (" __DATE__ " " __TIME__ ")"; }
+
+}  // extern "C"

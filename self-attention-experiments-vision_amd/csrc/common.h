@@ -1,0 +1,221 @@
+// common.h -- shared CDNA4 (gfx950) building blocks for the attention kernels.
+//
+// MFMA engine abstraction.  Every product in the kernels is a 32x32 MFMA tile:
+//   bf16: v_mfma_f32_32x32x16_bf16   (K = 16 per instruction, 8 elements per lane)
+//   f32 : v_mfma_f32_32x32x2_f32     (K = 2  per instruction, 1 element per lane; exact f32)
+// Operand maps (cdna_hip_programming.md §3): lane l = 32*h + r holds A[row r][k] and
+// B[k][col r] for k = KSTEP*s + KH*h + j (j < KH).  The accumulator has col = lane & 31 and
+// row = row_of(reg, h) = (reg & 3) + 8*(reg >> 2) + 4*h.
+//
+// "Accumulator as operand": a 32x32 accumulator X (col on the lane, rows in registers) is fed
+// to the next MFMA as the operand whose K index runs over X's rows without any lane movement.
+// K-step s, element j then carries X row row_of(KH*s + j, h); the other operand must supply the
+// same permuted K order -- colfrag() below reads it that way.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sae {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kInf = __builtin_huge_valf();
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float lg2(float x) { return __builtin_amdgcn_logf(x); }
+
+__device__ __forceinline__ int row_of(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+template <typename T> struct MF;
+
+template <> struct MF<__bf16> {
+  static constexpr int KSTEP = 16;
+  static constexpr int KH = 8;
+  using frag = bf16x8;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag zero() { return frag{}; }
+};
+
+template <> struct MF<float> {
+  static constexpr int KSTEP = 2;
+  static constexpr int KH = 1;
+  using frag = float;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag zero() { return 0.f; }
+};
+
+__device__ __forceinline__ f32x16 zero16() { return f32x16{}; }
+
+// ------------------------------------------------------------------------------ LDS images
+// bf16 tiles are [rows][DP] with 16-byte chunks XOR-swizzled per row so that both the
+// ds_read_b128 row reads (MFMA row operand) and the ds_read_b64_tr_b16 column reads
+// (accumulator-as-operand partner) are bank-conflict free:
+//   DP=32  (64-B rows) : swz = (r>>2)&3
+//   DP=64  (128-B rows): swz = bitreverse3((r>>1)&7)  -- rows r, r+2 land in opposite 64-B halves
+//   DP=128 (256-B rows): swz = ((r&3)<<2) | ((r>>2)&3)
+// f32 tiles are [rows][DP+1] floats (odd stride: conflict-free scalar row and column reads).
+template <int DP> __device__ __forceinline__ int swz(int r) {
+  if constexpr (DP == 32) return (r >> 2) & 3;
+  else if constexpr (DP == 64) return (((r >> 1) & 1) << 2) | (((r >> 2) & 1) << 1) | ((r >> 3) & 1);
+  else return ((r & 3) << 2) | ((r >> 2) & 3);
+}
+
+template <typename T, int DP> struct Img {
+  static constexpr int bytes(int rows) {
+    return sizeof(T) == 2 ? rows * DP * 2 : rows * (DP + 1) * 4;
+  }
+  // operand with the tile row on the lane and K over the head dim: element (r, KSTEP*s + KH*h + j)
+  static __device__ __forceinline__ typename MF<T>::frag rowfrag(const char* lds, int r, int s, int h) {
+    if constexpr (sizeof(T) == 2) {
+      const int c = 2 * s + h;
+      return *reinterpret_cast<const bf16x8*>(lds + r * (DP * 2) + 16 * (c ^ swz<DP>(r)));
+    } else {
+      return reinterpret_cast<const float*>(lds)[r * (DP + 1) + 2 * s + h];
+    }
+  }
+  // operand with the head-dim column (col0 + (lane&31)) on the lane and K over tile rows
+  // rowbase + row_of(KH*s + j, h): the partner of an accumulator fed as an operand.
+  static __device__ __forceinline__ typename MF<T>::frag colfrag(const char* lds, int rowbase, int s,
+                                                                   int col0, int lane) {
+    if constexpr (sizeof(T) == 2) {
+      const int li = lane & 15, g = lane >> 4, h = lane >> 5;
+      const int colb = col0 + 16 * (g & 1) + 4 * (li & 3);
+      const int chunk = colb >> 3, half = (colb >> 2) & 1;
+      const int r1 = rowbase + 16 * s + 4 * h + (li >> 2);
+      const int r2 = r1 + 8;
+      const char* p1 = lds + r1 * (DP * 2) + 16 * (chunk ^ swz<DP>(r1)) + 8 * half;
+      const char* p2 = lds + r2 * (DP * 2) + 16 * (chunk ^ swz<DP>(r2)) + 8 * half;
+      s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+      s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    } else {
+      const int h = lane >> 5;
+      return reinterpret_cast<const float*>(lds)[(rowbase + row_of(s, h)) * (DP + 1) + col0 + (lane & 31)];
+    }
+  }
+};
+
+// accumulator registers KH*s .. KH*s+KH-1 as an operand fragment
+template <typename T> __device__ __forceinline__ typename MF<T>::frag acc_frag(const f32x16& acc, int s) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (__bf16)acc[8 * s + j];
+    return f;
+  } else {
+    return acc[s];
+  }
+}
+
+// ------------------------------------------------------------------ global -> LDS staging
+// A ROWS x DP tile of a token-major tensor (row stride `rs` elements), staged through
+// registers (issue early, write late).  VEC: 16-byte loads (D % (16/sizeof(T)) == 0 and
+// aligned strides); otherwise element loads.  Rows >= nrows and columns >= D are zero.
+template <typename T, int DP, int ROWS, bool VEC> struct Stage {
+  static constexpr int EPC = 16 / sizeof(T);
+  static constexpr int CPR = DP / EPC;
+  static constexpr int NCH = (ROWS * CPR + 255) / 256;
+  uint4 v[NCH];
+
+  __device__ __forceinline__ void load(const T* base, int row0, int nrows, long long rs, int D, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 256 * i;
+      const int r = id / CPR, c = id % CPR;
+      const int row = row0 + r;
+      if (id >= ROWS * CPR) { v[i] = uint4{0, 0, 0, 0}; continue; }
+      if constexpr (VEC) {
+        if (row < nrows && c * EPC < D)
+          v[i] = *reinterpret_cast<const uint4*>(base + (long long)row * rs + c * EPC);
+        else
+          v[i] = uint4{0, 0, 0, 0};
+      } else {
+        T tmp[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          const int d = c * EPC + e;
+          tmp[e] = (row < nrows && d < D) ? base[(long long)row * rs + d] : (T)0.f;
+        }
+        v[i] = *reinterpret_cast<const uint4*>(tmp);
+      }
+    }
+  }
+  __device__ __forceinline__ void write(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 256 * i;
+      if (id >= ROWS * CPR) continue;
+      const int r = id / CPR, c = id % CPR;
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(lds + r * (DP * 2) + 16 * (c ^ swz<DP>(r))) = v[i];
+      } else {
+        float* f = reinterpret_cast<float*>(lds) + r * (DP + 1) + c * 4;
+        f[0] = __uint_as_float(v[i].x);
+        f[1] = __uint_as_float(v[i].y);
+        f[2] = __uint_as_float(v[i].z);
+        f[3] = __uint_as_float(v[i].w);
+      }
+    }
+  }
+};
+
+// Operand fragment read straight from global memory: row `row` of a token-major tensor,
+// elements d = KSTEP*s + KH*h + j.
+template <typename T, bool VEC>
+__device__ __forceinline__ typename MF<T>::frag gfrag(const T* base, int row, int nrows, long long rs,
+                                                      int D, int s, int h) {
+  const int d0 = MF<T>::KSTEP * s + MF<T>::KH * h;
+  if constexpr (sizeof(T) == 2) {
+    if (row >= nrows) return bf16x8{};
+    const T* p = base + (long long)row * rs + d0;
+    if constexpr (VEC) {
+      if (d0 < D) return *reinterpret_cast<const bf16x8*>(p);
+      return bf16x8{};
+    } else {
+      bf16x8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (d0 + j < D) ? p[j] : (__bf16)0.f;
+      return f;
+    }
+  } else {
+    if (row >= nrows || d0 >= D) return 0.f;
+    return base[(long long)row * rs + d0];
+  }
+}
+
+// Store 4 consecutive head-dim values (d0..d0+3) of one row.
+template <typename T, bool VEC>
+__device__ __forceinline__ void store4(T* rowp, int d0, int D, float a, float b, float c, float d) {
+  if constexpr (VEC) {
+    if (d0 >= D) return;
+    if constexpr (sizeof(T) == 2) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+      *reinterpret_cast<bf16x4*>(rowp + d0) = v;
+    } else {
+      *reinterpret_cast<f32x4*>(rowp + d0) = f32x4{a, b, c, d};
+    }
+  } else {
+    const float x[4] = {a, b, c, d};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (d0 + e < D) rowp[d0 + e] = (T)x[e];
+  }
+}
+
+// exact integer key -> (row, col) split for key < 4096, width <= 64: (key * magic) >> 20
+__host__ __device__ inline int div_magic(int w) { return (int)((1u << 20) / (unsigned)w + 1u); }
+
+}  // namespace sae

@@ -1,0 +1,313 @@
+"""Autograd operators over the C ABI (include/sae_attn.h).
+
+Each ``torch.autograd.Function`` below is a thin host-side shim: it allocates outputs with
+the framework's caching allocator, fills an ``sae_attn_desc`` with the tensors' element
+strides, and calls the HIP library on the current stream.  Forward saves the log-sum-exp
+rows, never the [B, H, Nq, Nk] probabilities (the reference materialises them:
+models/layers/attentions/attention.py:41-58).
+
+Public functions
+  attention(q, k, v, scale, bias=None)         core of AttentionBlock (attention.py:39-58)
+  attention_packed(qkv, scale)                  same, q/k/v packed [B, N, 3, H, D] (one buffer,
+                                                one gradient buffer, no copies)
+  talking_heads_attention(q, k, v, th1, th2, scale)   attention.py:41-52 with talking_heads
+  relpos_bias(qhat, emb_h, emb_w, grid)         BoTNet RelativeLogits tables (botnet.py:70-141)
+  rotary(x, base=10000.)                        rotary embedding (position_embed.py:8-20)
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib as L
+
+__all__ = ["attention", "attention_packed", "talking_heads_attention", "relpos_bias", "rotary",
+           "rotary_tables", "dtype_code"]
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return L.SAE_DTYPE_BF16
+    if dt == torch.float32:
+        return L.SAE_DTYPE_F32
+    raise TypeError(f"sae_vision_amd kernels take bfloat16 or float32, got {dt}")
+
+
+def _require_gpu(*ts: torch.Tensor):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("sae_vision_amd attention runs on the GPU only (HIP kernels); "
+                               f"got a tensor on {t.device}")
+
+
+def _bnh(t: torch.Tensor):
+    if t.dim() != 4:
+        raise ValueError(f"expected a [B, N, H, D] tensor, got shape {tuple(t.shape)}")
+    if t.stride(3) != 1:
+        raise ValueError("head_dim must be the innermost (stride-1) dimension")
+    return (t.stride(0), t.stride(1), t.stride(2))
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _make_desc(q, k, v, o, scale, dout=None, dq=None, dk=None, dv=None, grid=None) -> L.SaeAttnDesc:
+    lib = L.load()
+    B, Nq, H, D = q.shape
+    Nk = k.shape[1]
+    if k.shape != (B, Nk, H, D) or v.shape != (B, Nk, H, D):
+        raise ValueError(f"q {tuple(q.shape)} / k {tuple(k.shape)} / v {tuple(v.shape)} mismatch")
+    if not (q.dtype == k.dtype == v.dtype):
+        raise TypeError("q, k and v must share a dtype")
+    d = L.SaeAttnDesc()
+    lib.sae_attn_desc_init(ctypes.byref(d), B, H, Nq, Nk, D, dtype_code(q.dtype), float(scale))
+    d.q_stride, d.k_stride, d.v_stride = L.s3(_bnh(q)), L.s3(_bnh(k)), L.s3(_bnh(v))
+    if o is not None:
+        d.o_stride = L.s3(_bnh(o))
+    if dout is not None:
+        d.do_stride, d.dq_stride = L.s3(_bnh(dout)), L.s3(_bnh(dq))
+        d.dk_stride, d.dv_stride = L.s3(_bnh(dk)), L.s3(_bnh(dv))
+    if grid is not None:
+        d.flags = L.SAE_FLAG_RELPOS
+        d.rel_h, d.rel_w = int(grid[0]), int(grid[1])
+    return d
+
+
+def _fwd(q, k, v, scale, bias_h=None, bias_w=None, grid=None):
+    lib = L.load()
+    B, Nq, H, D = q.shape
+    o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
+    d = _make_desc(q, k, v, o, scale, grid=grid)
+    L.check(lib.sae_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(bias_h),
+                             _ptr(bias_w), _ptr(o), _ptr(lse)))
+    return o, lse
+
+
+def _bwd(q, k, v, o, lse, do, dq, dk, dv, scale, bias_h=None, bias_w=None, grid=None):
+    lib = L.load()
+    d = _make_desc(q, k, v, o, scale, do, dq, dk, dv, grid=grid)
+    ws = torch.empty(lib.sae_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
+    dbh = dbw = None
+    if grid is not None:
+        dbh, dbw = torch.empty_like(bias_h), torch.empty_like(bias_w)
+    L.check(lib.sae_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse),
+                             _ptr(do), _ptr(bias_h), _ptr(bias_w), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dbh),
+                             _ptr(dbw), _ptr(ws)))
+    return dbh, dbw
+
+
+def _grad_in(g: torch.Tensor) -> torch.Tensor:
+    return g if g.stride(-1) == 1 else g.contiguous()
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, bias_h, bias_w, grid):
+        _require_gpu(q, k, v)
+        o, lse = _fwd(q, k, v, scale, bias_h, bias_w, grid)
+        ctx.save_for_backward(q, k, v, o, lse, bias_h, bias_w)
+        ctx.scale, ctx.grid = scale, grid
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, bias_h, bias_w = ctx.saved_tensors
+        do = _grad_in(do)
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        dbh, dbw = _bwd(q, k, v, o, lse, do, dq, dk, dv, ctx.scale, bias_h, bias_w, ctx.grid)
+        return dq, dk, dv, None, dbh, dbw, None
+
+
+class _AttentionPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, scale):
+        _require_gpu(qkv)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o, lse = _fwd(q, k, v, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        do = _grad_in(do)
+        dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        _bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
+             ctx.scale)
+        return dqkv, None
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,
+              bias: Optional[Tuple[torch.Tensor, torch.Tensor, Tuple[int, int]]] = None) -> torch.Tensor:
+    """softmax(scale * q k^T [+ relpos bias]) v on token-major [B, N, H, D] tensors.
+
+    ``scale`` defaults to the reference's 1/sqrt(head_ch) (attention.py:39).  ``bias`` is
+    ``(bias_h, bias_w, (Hs, Ws))`` from :func:`relpos_bias` (BoTNet)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if bias is None:
+        return _Attention.apply(q, k, v, float(scale), None, None, None)
+    bh, bw, grid = bias
+    return _Attention.apply(q, k, v, float(scale), bh, bw, tuple(grid))
+
+
+def attention_packed(qkv: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
+    """Self-attention on a packed projection ``qkv`` [B, N, 3, H, D] (one fused QKV GEMM output)."""
+    if qkv.dim() != 5 or qkv.shape[2] != 3:
+        raise ValueError(f"expected qkv [B, N, 3, H, D], got {tuple(qkv.shape)}")
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    return _AttentionPacked.apply(qkv, float(scale))
+
+
+# ----------------------------------------------------------------------------- talking heads
+class _TalkingHeads(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, th1, th2, scale):
+        _require_gpu(q, k, v, th1, th2)
+        lib = L.load()
+        B, Nq, H, D = q.shape
+        th1c = th1.detach().to(torch.float32).contiguous()
+        th2c = th2.detach().to(torch.float32).contiguous()
+        o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
+        lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
+        d = _make_desc(q, k, v, o, scale)
+        L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
+                                    _ptr(th2c), _ptr(o), _ptr(lse)))
+        ctx.save_for_backward(q, k, v, th1c, th2c, lse)
+        ctx.scale = scale
+        ctx.th_dtypes = (th1.dtype, th2.dtype)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, th1, th2, lse = ctx.saved_tensors
+        lib = L.load()
+        do = _grad_in(do)
+        dq, dk, dv = (torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in (q, k, v))
+        dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
+        d = _make_desc(q, k, v, None, ctx.scale, do, dq, dk, dv)
+        ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
+        L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
+                                    _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
+                                    _ptr(ws)))
+        return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
+
+
+def talking_heads_attention(q, k, v, th1, th2, scale: Optional[float] = None):
+    """Talking-heads attention (attention.py:41-58, talking_heads.py:9-14); th1/th2 are the
+    fp32 [H, H] ``talking_heads_transform`` params of TalkingHeadsBlock_0 / _1."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    return _TalkingHeads.apply(q, k, v, th1, th2, float(scale))
+
+
+# ------------------------------------------------------------------------ relative logits
+class _RelposBias(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qhat, emb_h, emb_w, Hs, Ws):
+        _require_gpu(qhat, emb_h, emb_w)
+        lib = L.load()
+        B, N, H, D = qhat.shape
+        if N != Hs * Ws:
+            raise ValueError(f"relpos grid {Hs}x{Ws} does not match {N} tokens")
+        eh = emb_h.detach().to(torch.float32).contiguous()
+        ew = emb_w.detach().to(torch.float32).contiguous()
+        bh = torch.empty((B, H, N, Hs), dtype=torch.float32, device=qhat.device)
+        bw = torch.empty((B, H, N, Ws), dtype=torch.float32, device=qhat.device)
+        L.check(lib.sae_relpos_bias_fwd(_stream(qhat), B, H, Hs, Ws, D, dtype_code(qhat.dtype), _ptr(qhat),
+                                        L.s3(_bnh(qhat)), _ptr(eh), _ptr(ew), _ptr(bh), _ptr(bw)))
+        ctx.save_for_backward(qhat, eh, ew)
+        ctx.grid = (Hs, Ws)
+        ctx.emb_dtypes = (emb_h.dtype, emb_w.dtype)
+        return bh, bw
+
+    @staticmethod
+    def backward(ctx, dbh, dbw):
+        qhat, eh, ew = ctx.saved_tensors
+        lib = L.load()
+        Hs, Ws = ctx.grid
+        B, N, H, D = qhat.shape
+        dbh = dbh.contiguous() if dbh is not None else torch.zeros((B, H, N, Hs), device=qhat.device)
+        dbw = dbw.contiguous() if dbw is not None else torch.zeros((B, H, N, Ws), device=qhat.device)
+        dq = torch.empty((B, N, H, D), dtype=qhat.dtype, device=qhat.device)
+        deh, dew = torch.empty_like(eh), torch.empty_like(ew)
+        ws = torch.empty(lib.sae_relpos_bias_bwd_workspace_bytes(B, Hs, Ws, D), dtype=torch.uint8,
+                         device=qhat.device)
+        L.check(lib.sae_relpos_bias_bwd(_stream(qhat), B, H, Hs, Ws, D, dtype_code(qhat.dtype), _ptr(qhat),
+                                        L.s3(_bnh(qhat)), _ptr(eh), _ptr(ew), _ptr(dbh), _ptr(dbw), None, _ptr(dq),
+                                        L.s3(_bnh(dq)), _ptr(deh), _ptr(dew), _ptr(ws)))
+        return dq, deh.to(ctx.emb_dtypes[0]), dew.to(ctx.emb_dtypes[1]), None, None
+
+
+def relpos_bias(qhat, emb_h, emb_w, grid: Tuple[int, int]):
+    """BoTNet RelativeLogits (botnet.py:113-141) as two fp32 tables per query row:
+    bias_h [B,H,N,Hs], bias_w [B,H,N,Ws]; the attention kernel adds
+    ``bias_h[q, k // Ws] + bias_w[q, k % Ws]`` to the score tile."""
+    return _RelposBias.apply(qhat, emb_h, emb_w, int(grid[0]), int(grid[1]))
+
+
+# ---------------------------------------------------------------------------------- rotary
+_TABLES = {}
+
+
+def rotary_tables(n: int, dim: int, device, base: float = 10000.0):
+    """fp32 sin/cos tables [n, dim/2] computed in float64 on the host (exact angles for the
+    long CvT sequences; device sinf at |theta| ~ 3e3 would lose ~1e-4)."""
+    key = (n, dim, float(base), str(device))
+    t = _TABLES.get(key)
+    if t is None:
+        i = torch.arange(dim // 2, dtype=torch.float64)
+        inv_freq = base ** (-2.0 * i / dim)
+        ang = torch.arange(n, dtype=torch.float64)[:, None] * inv_freq[None, :]
+        t = (torch.sin(ang).float().to(device), torch.cos(ang).float().to(device))
+        _TABLES[key] = t
+    return t
+
+
+def _rotary_call(x, y, sin, cos, inverse):
+    lib = L.load()
+    B, N, H, D = x.shape
+    L.check(lib.sae_rotary(_stream(x), B, N, H, D, dtype_code(x.dtype), _ptr(x), L.s3(_bnh(x)), _ptr(y),
+                           L.s3(_bnh(y)), _ptr(sin), _ptr(cos), 1 if inverse else 0))
+
+
+class _Rotary(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, base):
+        _require_gpu(x)
+        B, N, H, D = x.shape
+        if D % 2:
+            raise ValueError("rotary needs an even head_dim")
+        sin, cos = rotary_tables(N, D, x.device, base)
+        y = torch.empty((B, N, H, D), dtype=x.dtype, device=x.device)
+        _rotary_call(x, y, sin, cos, False)
+        ctx.base = base
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = _grad_in(dy)
+        B, N, H, D = dy.shape
+        sin, cos = rotary_tables(N, D, dy.device, ctx.base)
+        dx = torch.empty((B, N, H, D), dtype=dy.dtype, device=dy.device)
+        _rotary_call(dy, dx, sin, cos, True)
+        return dx, None
+
+
+def rotary(x: torch.Tensor, base: float = 10000.0) -> torch.Tensor:
+    """GPT-J interleaved rotary on [B, N, H, D] (position_embed.py:8-20; build-defined base
+    10000, survey D6)."""
+    return _Rotary.apply(x, float(base))

@@ -1,0 +1,142 @@
+"""GPU parity of the fused attention core (sae_attn_fwd / sae_attn_bwd through the C ABI)
+against the CPU oracle (oracle/attention_ref.py restating attention.py:39-58).
+
+Tolerances (north_star): fp32 max|a-b|/max|ref| <= 1e-5, bf16 <= 2e-2.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import attention_ref as R
+from _util import TOL, randn, rel_err
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # B, Nq, Nk, H, D, mode                       what it covers
+    (2, 17, 17, 3, 64, "f32"),                   # tiny, ragged tiles
+    (2, 197, 197, 6, 64, "bf16"),                # DeiT-S layer
+    (2, 197, 197, 6, 64, "f32"),
+    (1, 577, 577, 2, 64, "bf16"),                # ViT-B/16@384 (N >= 577)
+    (2, 196, 196, 8, 48, "bf16"),                # CaiT-S24 head dim 48
+    (2, 196, 196, 8, 48, "f32"),                 # CaiT trunk runs fp32 (survey D7)
+    (1, 49, 49, 4, 128, "bf16"),                 # BoTNet 7x7, D = 128
+    (1, 49, 49, 4, 128, "f32"),
+    (3, 16, 16, 4, 10, "f32"),                   # TNT inner attention, D = 10 (scalar path)
+    (3, 16, 16, 4, 6, "bf16"),                   # TNT-B inner, D = 6
+    (2, 1, 197, 8, 48, "bf16"),                  # CaiT class attention (Nq = 1)
+    (2, 1, 12, 3, 64, "f32"),                    # CeiT LCA (Nq = 1, Nk = 12)
+    (2, 100, 37, 3, 32, "bf16"),                 # CvT-style Nq != Nk
+    (1, 1, 1, 1, 64, "f32"),                     # single key
+    (1, 129, 65, 1, 64, "f32"),                  # tile boundaries + 1
+]
+
+
+def _torch_dtype(mode):
+    import torch
+    return torch.bfloat16 if mode == "bf16" else torch.float32
+
+
+@pytest.mark.parametrize("B,Nq,Nk,H,D,mode", CASES)
+def test_attention_fwd_bwd(dev, B, Nq, Nk, H, D, mode):
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(0)
+    q, k, v = (randn(rng, (B, n, H, D), mode) for n in (Nq, Nk, Nk))
+    do = randn(np.random.default_rng(2), (B, Nq, H, D), mode)
+    td = _torch_dtype(mode)
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=td, requires_grad=True) for x in (q, k, v))
+    o = ops.attention(tq, tk, tv)
+    o.backward(torch.tensor(do, device=dev, dtype=td))
+    torch.cuda.synchronize()
+
+    o_ref = R.attention_core_fwd(q, k, v, mode)
+    assert rel_err(o, o_ref) <= TOL[mode]
+    g = R.attention_core_bwd(q, k, v, do)
+    for name, t in (("dq", tq), ("dk", tk), ("dv", tv)):
+        err = rel_err(t.grad, g[name])
+        assert err <= TOL[mode], f"{name}: rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_lse_matches_oracle(dev, mode):
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(0)
+    B, N, H, D = 2, 197, 3, 64
+    q, k, v = (randn(rng, (B, N, H, D), mode) for _ in range(3))
+    td = _torch_dtype(mode)
+    o, lse = ops._fwd(*(torch.tensor(x, device=dev, dtype=td) for x in (q, k, v)), 1.0 / math.sqrt(D))
+    _, aux = R.attention_core_fwd(q, k, v, "f64", return_aux=True)
+    np.testing.assert_allclose(lse.cpu().numpy(), aux["lse"], rtol=0, atol=1e-4 if mode == "f32" else 2e-2)
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_packed_qkv_strided(dev, mode):
+    """q/k/v read in place from a packed [B, N, 3, H, D] projection (strided descriptor)."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(1)
+    B, N, H, D = 2, 197, 6, 64
+    qkv = randn(rng, (B, N, 3, H, D), mode)
+    do = randn(np.random.default_rng(2), (B, N, H, D), mode)
+    td = _torch_dtype(mode)
+    t = torch.tensor(qkv, device=dev, dtype=td, requires_grad=True)
+    o = ops.attention_packed(t)
+    o.backward(torch.tensor(do, device=dev, dtype=td))
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    assert rel_err(o, R.attention_core_fwd(q, k, v, mode)) <= TOL[mode]
+    g = R.attention_core_bwd(q, k, v, do)
+    gg = t.grad
+    for i, name in enumerate(("dq", "dk", "dv")):
+        assert rel_err(gg[:, :, i], g[name]) <= TOL[mode], name
+
+
+def test_deterministic(dev):
+    """Backward has no HBM atomics: two runs are bitwise identical."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q, k, v = (torch.randn(2, 197, 6, 64, generator=g).to(dev, torch.bfloat16).requires_grad_() for _ in range(3))
+    do = torch.randn(2, 197, 6, 64, generator=g).to(dev, torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        for t in (q, k, v):
+            t.grad = None
+        o = ops.attention(q, k, v)
+        o.backward(do)
+        outs.append([o.detach().clone()] + [t.grad.clone() for t in (q, k, v)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_softmax_spike(dev):
+    """Forces the online-softmax rescale: one key dominates at a late tile (rule 26)."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(5)
+    B, N, H, D = 1, 300, 2, 64
+    q = rng.standard_normal((B, N, H, D)).astype(np.float32)
+    k = rng.standard_normal((B, N, H, D)).astype(np.float32)
+    v = rng.standard_normal((B, N, H, D)).astype(np.float32)
+    k[0, 250] = q[0, 7] * 4.0          # spike for query 7 in the 4th key tile
+    k[0, 0] = -q[0, 7] * 3.0
+    o = ops.attention(*(torch.tensor(x, device=dev) for x in (q, k, v)))
+    assert rel_err(o.cpu().numpy(), R.attention_core_fwd(q, k, v, "f64")) <= TOL["f32"]
+
+
+def test_error_reporting(dev):
+    """Invalid descriptors fail loudly with the C ABI's message."""
+    import torch
+    import sae_vision_amd.ops as ops
+    from sae_vision_amd import SaeError
+
+    q = torch.zeros(1, 4, 1, 256, device=dev)
+    with pytest.raises(SaeError, match="head_dim 256"):
+        ops.attention(q, q, q)
