@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: DeiT-S/16 224px bf16 data-parallel training on MI355X (BASELINE.json configs[1]
+at N=1, configs[2]-style DP scaling at N>1) with the fused HIP attention on the hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One process per GPU; the batch (128 images per GPU, synthetic N(0,1) images + uniform labels,
+resident in HBM) is sharded across ranks, gradients are all-reduced over RCCL (DDP buckets
+overlapped with the backward).  W untimed warm-up steps, then exactly K steps bracketed by a
+barrier + device synchronisation on both sides; the max elapsed time over ranks is used.
+Rank 0 prints ONE JSON line:
+  value        = whole-job training images/s (all ranks)
+  roofline     = the fused attention op of this workload (fwd + bwd = 4 launches: attn_fwd,
+                 attn_bwd_delta, attn_bwd_dkdv, attn_bwd_dq), timed live with HIP events on its
+                 launch stream inside the timed region; algorithmic FLOPs/bytes per call
+  cpu_baseline = the numpy port (oracle/vit_ref.py) of the same training step on a bounded
+                 sample, on this host's cores (rank 0, N=1 only)
+  attention_headline = the fused fwd+bwd core alone at ViT-B/16@384 shape (B=64, N=577, H=12,
+                 D=64), TFLOP/s and fraction of the 2.5 PF bf16 MFMA peak (N>=577 target)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "attention fwd+bwd TFLOP/s (% MFMA peak); DeiT-S/16 train img/s at 1/8 GPUs"
+PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
+RIDGE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def attn_work(B, Nq, Nk, H, D, elt=2):
+    """Algorithmic FLOPs / HBM bytes of one fused attention call."""
+    f_fwd = 4.0 * B * H * Nq * Nk * D
+    f_bwd = 8.0 * B * H * Nq * Nk * D
+    b_fwd = elt * B * H * D * (2 * Nq + 2 * Nk) + 4.0 * B * H * Nq
+    b_bwd = elt * B * H * D * (4 * Nq + 4 * Nk) + 8.0 * B * H * Nq
+    return f_fwd, f_bwd, b_fwd, b_bwd
+
+
+def roofline_entry(flops, nbytes, seconds, traffic=None):
+    ai = flops / nbytes
+    if ai >= RIDGE:
+        ach, peak, unit, bound = flops / seconds / 1e12, PEAK_BF16_TFLOPS, "TFLOP/s", "mfma"
+    else:
+        ach, peak, unit, bound = nbytes / seconds / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    return {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+            "traffic": traffic, "algorithmic_flops": flops, "algorithmic_bytes": nbytes,
+            "arith_intensity": round(ai, 1), "tflops": round(flops / seconds / 1e12, 2),
+            "gbs": round(nbytes / seconds / 1e9, 1), "ms_per_call": round(seconds * 1e3, 4)}
+
+
+def load_traffic(name):
+    """HBM bytes per call from the committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(name, {}).get("hbm_bytes_per_call")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(model_name, seconds_budget=15.0):
+    """numpy port of the training step (oracle/vit_ref.py) on a bounded sample."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vit_ref
+    from sae_vision_amd import vit
+    L, H, C, p = vit.MODEL_CONFIGS[model_name]
+    cpu_model = vit.create_model(model_name, 1000, torch.float32, device="cpu")
+    params = {k: v.detach().numpy().astype(np.float32).copy() for k, v in cpu_model.named_parameters()}
+    rng = np.random.default_rng(0)
+    bs = 2
+    images = rng.standard_normal((bs, 224, 224, 3)).astype(np.float32)
+    labels = rng.integers(0, 1000, size=bs)
+    state = {}
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = len(os.sched_getaffinity(0))
+    n_img, t0 = 0, time.perf_counter()
+    while True:
+        _, _, grads = vit_ref.vit_loss_and_grads(params, images, labels, L, H, p)
+        vit_ref.adam_update(params, grads, state)
+        n_img += bs
+        if time.perf_counter() - t0 > seconds_budget or n_img >= 16:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n_img / dt, 3), "unit": "img/s", "cores": int(cores), "kind": "port",
+            "sample": f"{model_name} fp32 numpy train step (fwd+loss+bwd+AdamW), batch {bs} x {n_img // bs} steps, "
+                      f"{dt:.1f} s"}
+
+
+def headline(dev, steps=20, warmup=5):
+    """Fused attention fwd+bwd alone at the ViT-B/16@384 shape, HIP events on its stream."""
+    import torch
+    import sae_vision_amd.ops as ops
+    B, N, H, D = 64, 577, 12, 64
+    g = torch.Generator(device=dev).manual_seed(0)
+    qkv = torch.randn(B, N, 3, H, D, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+    do = torch.randn(B, N, H, D, device=dev, generator=g).to(torch.bfloat16)
+    for _ in range(warmup):
+        ops.attention_packed(qkv).backward(do)
+    torch.cuda.synchronize()
+    t = ops.KernelTimer()
+    ops.set_kernel_timer(t)
+    for _ in range(steps):
+        ops.attention_packed(qkv).backward(do)
+    ops.set_kernel_timer(None)
+    s = t.summary()
+    f_fwd, f_bwd, b_fwd, b_bwd = attn_work(B, N, N, H, D)
+    sec = (s["attn_fwd"]["mean_ms"] + s["attn_bwd"]["mean_ms"]) / 1e3
+    r = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, sec, load_traffic("vitb384"))
+    return {"shape": {"B": B, "N": N, "H": H, "D": D}, "fwd_ms": round(s["attn_fwd"]["mean_ms"], 4),
+            "bwd_ms": round(s["attn_bwd"]["mean_ms"], 4), "fwd_tflops": round(f_fwd / s["attn_fwd"]["mean_ms"] / 1e9, 1),
+            "bwd_tflops": round(f_bwd / s["attn_bwd"]["mean_ms"] / 1e9, 1), "tflops": r["tflops"],
+            "frac_mfma_peak": round(r["tflops"] / PEAK_BF16_TFLOPS, 4), "roofline": r}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--model", default="deit_s_patch16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-headline", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="training loop only (for rocprofv3 runs)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import sae_vision_amd
+    from sae_vision_amd import ops, train, vit
+
+    rank, world, local = train.init_distributed()
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    dev = torch.device("cuda", local)
+    sae_vision_amd.load_library()
+
+    torch.manual_seed(0)
+    model = vit.create_model(args.model, 1000, torch.bfloat16, device=dev)
+    B = args.batch
+    step = train.TrainStep(model, global_batch=B * world, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    images = torch.randn(B, 224, 224, 3, device=dev, generator=g)
+    labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
+
+    for _ in range(args.warmup):
+        step(images, labels)
+    torch.cuda.synchronize()
+    timer = ops.KernelTimer()
+    ops.set_kernel_timer(timer)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(images, labels)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    ksum = timer.summary()
+    L, Hh, C, p = vit.MODEL_CONFIGS[args.model]
+    N = (224 // p) ** 2 + 1
+    D = C // Hh
+    f_fwd, f_bwd, b_fwd, b_bwd = attn_work(B, N, N, Hh, D)
+    fwd_ms, bwd_ms = ksum["attn_fwd"]["mean_ms"], ksum["attn_bwd"]["mean_ms"]
+    roof = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, (fwd_ms + bwd_ms) / 1e3, load_traffic("deit_s"))
+    img_s = B * world * args.steps / elapsed
+    flop_img = 3 * vit.vit_flops_per_image(args.model)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+        return
+    out = {
+        "metric": METRIC, "value": round(img_s, 2), "unit": "img/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"DeiT-S/16 224px bf16 data-parallel training step (fused attention fwd+bwd)",
+                   "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
+                   "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "attention": {"calls_per_step": ksum["attn_fwd"]["launches"] // args.steps, "fwd_ms": round(fwd_ms, 4),
+                      "bwd_ms": round(bwd_ms, 4), "tflops": roof["tflops"],
+                      "share_of_step": round((fwd_ms + bwd_ms) * ksum["attn_fwd"]["launches"] / args.steps
+                                             / (elapsed / args.steps * 1e3), 4)},
+        "e2e": {"train_flop_per_img": flop_img, "tflops": round(img_s * flop_img / 1e12, 1),
+                "mfma_frac": round(img_s * flop_img / 1e12 / (world * PEAK_BF16_TFLOPS), 4),
+                "final_loss": round(final_loss, 4)},
+    }
+    if not args.profile and not args.no_headline:
+        out["attention_headline"] = headline(dev)
+    if not args.profile and not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(args.model)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,43 @@ import torch
 from . import _lib as L
 
 __all__ = ["attention", "attention_packed", "talking_heads_attention", "relpos_bias", "rotary",
-           "rotary_tables", "dtype_code"]
+           "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
+
+
+class KernelTimer:
+    """Brackets every C-ABI launch group with HIP events on the launch stream (used by
+    bench.py to time the fused kernels inside the timed region of a training step)."""
+
+    def __init__(self):
+        self.events = {}
+
+    def begin(self, name):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+        return name, e0
+
+    def end(self, token, work=None):
+        name, e0 = token
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream())
+        self.events.setdefault(name, []).append((e0, e1, work))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, lst in self.events.items():
+            ms = [a.elapsed_time(b) for a, b, _ in lst]
+            out[name] = {"launches": len(ms), "total_ms": sum(ms), "mean_ms": sum(ms) / max(1, len(ms)),
+                         "work": [w for _, _, w in lst]}
+        return out
+
+
+_TIMER = None
+
+
+def set_kernel_timer(t):
+    global _TIMER
+    _TIMER = t
 
 
 def dtype_code(dt: torch.dtype) -> int:
@@ -87,8 +123,11 @@ def _fwd(q, k, v, scale, bias_h=None, bias_w=None, grid=None):
     o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
     lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
     d = _make_desc(q, k, v, o, scale, grid=grid)
+    tok = _TIMER.begin("attn_fwd") if _TIMER is not None else None
     L.check(lib.sae_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(bias_h),
                              _ptr(bias_w), _ptr(o), _ptr(lse)))
+    if tok is not None:
+        _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
     return o, lse
 
 
@@ -99,9 +138,12 @@ def _bwd(q, k, v, o, lse, do, dq, dk, dv, scale, bias_h=None, bias_w=None, grid=
     dbh = dbw = None
     if grid is not None:
         dbh, dbw = torch.empty_like(bias_h), torch.empty_like(bias_w)
+    tok = _TIMER.begin("attn_bwd") if _TIMER is not None else None
     L.check(lib.sae_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse),
                              _ptr(do), _ptr(bias_h), _ptr(bias_w), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dbh),
                              _ptr(dbw), _ptr(ws)))
+    if tok is not None:
+        _TIMER.end(tok, tuple(q.shape[:2]) + (k.shape[1],) + tuple(q.shape[2:]))
     return dbh, dbw
 
 

@@ -1,0 +1,75 @@
+"""Data-parallel training step (train.py:77-109 of the reference, rebuilt for MI355X).
+
+One process per GPU, ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm) over
+xGMI.  The reference's ``jax.pmap(train_step)`` + ``lax.pmean(grads)`` (train.py:94-96,230)
+becomes DistributedDataParallel: fp32 gradients are all-reduced in size-capped buckets in
+reverse layer order on RCCL's own stream while the backward pass is still running (the
+overlap the reference lacks, survey §3.2).  Survey D9 decisions: standard descent (the
+reference's optax chain ascends), the gradient is the global batch mean (the reference
+divides the loss by device_count *and* pmean's), no wandb call inside the step.
+
+Loss: one-hot -> optax.smooth_labels(0.1) -> softmax cross-entropy, mean (train.py:83-92).
+Optimizer: Adam + decoupled weight decay 1e-4, lr 5e-4 * batch/512 (train.py:25-27,229-233;
+constant schedule: the warmup-cosine value does not change the work per step).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+__all__ = ["smoothed_cross_entropy", "TrainStep", "init_distributed"]
+
+
+def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.1) -> torch.Tensor:
+    return F.cross_entropy(logits.float(), labels, label_smoothing=smoothing)
+
+
+def init_distributed():
+    """Initialise the process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+class TrainStep:
+    """``step(images, labels)`` = forward (bf16 compute) + loss + backward (+ bucketed RCCL
+    all-reduce overlapped with it when world > 1) + optimizer update.  No host sync."""
+
+    def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
+                 label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None):
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.model = model
+        if self.world > 1:
+            self.ddp = torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[device.index] if (device is not None and device.type == "cuda") else None,
+                bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
+        else:
+            self.ddp = model
+        base_lr = lr * (global_batch / 512)
+        params = [p for p in model.parameters() if p.requires_grad]
+        kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
+        try:
+            self.opt = torch.optim.AdamW(params, fused=True, **kw)
+        except (RuntimeError, TypeError):
+            self.opt = torch.optim.AdamW(params, foreach=True, **kw)
+        self.smoothing = label_smoothing
+
+    def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        self.opt.zero_grad(set_to_none=True)
+        logits = self.ddp(images, is_training=True)
+        loss = smoothed_cross_entropy(logits, labels, self.smoothing)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()

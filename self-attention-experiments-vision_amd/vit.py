@@ -1,0 +1,163 @@
+"""ViT / DeiT -- the caller of the attention hot path used for the end-to-end img/s metric.
+
+Mirrors models/vit.py:9-99 (EncoderBlock, Encoder, ViT), models/layers/stems/patch_embed.py:8-26
+(PatchEmbedBlock), models/layers/feedforwards/ff.py:8-34 (FFBlock) and
+models/layers/position_embed.py:48-57 (AddAbsPosEmbed), with Flax-style submodule names so
+the parameter tree matches (``PatchEmbedBlock_0/Dense_0/kernel``, ``cls``,
+``Encoder_0/EncoderBlock_i/SelfAttentionBlock_0/queries/kernel``, ...).  Numerics follow the
+reference's mixed precision: fp32 params, ``dtype`` compute, fp32 residual stream (the fp32
+cls / pos-embed params promote it, vit.py:46,85), LayerNorm eps 1e-6, tanh-GELU (Flax
+``nn.gelu`` default).
+
+The attention is ``layers.SelfAttentionBlock`` (fused HIP kernels); LayerNorm, GELU and the
+Dense GEMMs are library ops (survey §8f ranks them "next").
+"""
+from __future__ import annotations
+
+import math
+from typing import Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .layers.attention import DenseGeneral, SelfAttentionBlock, lecun_normal_
+
+__all__ = ["ViT", "create_model", "MODEL_CONFIGS", "vit_flops_per_image"]
+
+
+class Dense(nn.Module):
+    """Flax ``nn.Dense`` param holder (kernel [in, out] lecun_normal, bias zeros)."""
+
+    def __init__(self, in_features, features, use_bias=True, zero_init=False, device=None):
+        super().__init__()
+        k = torch.zeros(in_features, features, device=device)
+        if not zero_init:
+            lecun_normal_(k, in_features)
+        self.kernel = nn.Parameter(k)
+        self.bias = nn.Parameter(torch.zeros(features, device=device)) if use_bias else None
+
+    def forward(self, x, dtype):
+        y = x.to(dtype) @ self.kernel.to(dtype)
+        return y + self.bias.to(dtype) if self.bias is not None else y
+
+
+class LayerNorm(nn.Module):
+    """Flax ``nn.LayerNorm(dtype)``: params ``scale`` / ``bias``, eps 1e-6, output in dtype."""
+
+    def __init__(self, dim, device=None):
+        super().__init__()
+        self.scale = nn.Parameter(torch.ones(dim, device=device))
+        self.bias = nn.Parameter(torch.zeros(dim, device=device))
+
+    def forward(self, x, dtype):
+        return F.layer_norm(x.float(), (x.shape[-1],), self.scale, self.bias, 1e-6).to(dtype)
+
+
+class FFBlock(nn.Module):
+    """ff.py:8-34 (expand_ratio, Dense -> GELU -> Dense, dropout 0)."""
+
+    def __init__(self, dim, expand_ratio=4, device=None):
+        super().__init__()
+        hid = max(1, int(expand_ratio * dim))
+        self.Dense_0 = Dense(dim, hid, device=device)
+        self.Dense_1 = Dense(hid, dim, device=device)
+
+    def forward(self, x, dtype):
+        return self.Dense_1(F.gelu(self.Dense_0(x, dtype), approximate="tanh"), dtype)
+
+
+class EncoderBlock(nn.Module):
+    """vit.py:9-32."""
+
+    def __init__(self, dim, num_heads, expand_ratio, dtype, device=None):
+        super().__init__()
+        self.dtype = dtype
+        self.LayerNorm_0 = LayerNorm(dim, device)
+        self.SelfAttentionBlock_0 = SelfAttentionBlock(num_heads=num_heads, dtype=dtype, in_ch=dim, device=device)
+        self.LayerNorm_1 = LayerNorm(dim, device)
+        self.FFBlock_0 = FFBlock(dim, expand_ratio, device)
+
+    def forward(self, inputs, is_training):
+        x = self.SelfAttentionBlock_0(self.LayerNorm_0(inputs, self.dtype), is_training=is_training)
+        x = x + inputs
+        y = self.FFBlock_0(self.LayerNorm_1(x, self.dtype), self.dtype)
+        return x + y
+
+
+class Encoder(nn.Module):
+    """vit.py:35-58 (AddAbsPosEmbed_0 + EncoderBlock_i + LayerNorm_0)."""
+
+    def __init__(self, num_tokens, dim, num_layers, num_heads, expand_ratio, dtype, device=None):
+        super().__init__()
+        self.dtype = dtype
+        self.AddAbsPosEmbed_0 = nn.Module()
+        self.AddAbsPosEmbed_0.pos_embed = nn.Parameter(torch.randn(1, num_tokens, dim, device=device) * 0.02)
+        for i in range(num_layers):
+            setattr(self, f"EncoderBlock_{i}", EncoderBlock(dim, num_heads, expand_ratio, dtype, device))
+        self.num_layers = num_layers
+        self.LayerNorm_0 = LayerNorm(dim, device)
+
+    def forward(self, inputs, is_training):
+        x = inputs.float() + self.AddAbsPosEmbed_0.pos_embed
+        for i in range(self.num_layers):
+            x = getattr(self, f"EncoderBlock_{i}")(x, is_training)
+        return self.LayerNorm_0(x, self.dtype)
+
+
+class ViT(nn.Module):
+    """vit.py:61-99.  ``forward(inputs [B, H, W, 3], is_training)`` -> logits [B, classes]."""
+
+    def __init__(self, num_classes: int, num_layers: int, num_heads: int, embed_dim: int,
+                 patch_shape: Tuple[int, int], img_size: int = 224, expand_ratio: float = 4,
+                 dtype: torch.dtype = torch.float32, device=None):
+        super().__init__()
+        assert embed_dim % num_heads == 0
+        self.patch_shape, self.dtype, self.embed_dim = tuple(patch_shape), dtype, embed_dim
+        ph, pw = self.patch_shape
+        self.PatchEmbedBlock_0 = nn.Module()
+        self.PatchEmbedBlock_0.Dense_0 = Dense(ph * pw * 3, embed_dim, use_bias=False, device=device)
+        self.cls = nn.Parameter(torch.zeros(1, 1, embed_dim, device=device))
+        n = (img_size // ph) * (img_size // pw) + 1
+        self.Encoder_0 = Encoder(n, embed_dim, num_layers, num_heads, expand_ratio, dtype, device)
+        self.Dense_0 = Dense(embed_dim, num_classes, zero_init=True, device=device)
+
+    def forward(self, inputs: torch.Tensor, is_training: bool) -> torch.Tensor:
+        b, H, W, c = inputs.shape
+        ph, pw = self.patch_shape
+        x = inputs.to(self.dtype).reshape(b, H // ph, ph, W // pw, pw, c).permute(0, 1, 3, 2, 4, 5)
+        x = x.reshape(b, (H // ph) * (W // pw), ph * pw * c)          # 'b (h ph) (w pw) c -> b (h w) (ph pw c)'
+        x = self.PatchEmbedBlock_0.Dense_0(x, self.dtype)
+        x = torch.cat([self.cls.expand(b, 1, self.embed_dim), x.float()], dim=1)   # fp32 (promotion)
+        x = self.Encoder_0(x, is_training)
+        return self.Dense_0(x[:, 0], self.dtype)
+
+
+# name -> (layers, heads, embed_dim, patch); create_model.py:10-37 plus the DeiT entries (survey D10)
+MODEL_CONFIGS = {
+    "vit_b_patch32": (12, 12, 768, 32),
+    "vit_b_patch16": (12, 12, 768, 16),
+    "vit_l_patch32": (24, 16, 1024, 32),
+    "vit_l_patch16": (24, 16, 1024, 16),
+    "deit_ti_patch16": (12, 3, 192, 16),
+    "deit_s_patch16": (12, 6, 384, 16),
+}
+
+
+def create_model(model_name: str, num_classes: int = 1000, dtype: torch.dtype = torch.float32,
+                 img_size: int = 224, device=None) -> ViT:
+    """``create_model`` (models/create_model.py:6-215) for the ViT/DeiT family."""
+    if model_name not in MODEL_CONFIGS:
+        raise ValueError(f"unknown model {model_name!r}; ViT/DeiT family: {sorted(MODEL_CONFIGS)}")
+    L, Hh, C, p = MODEL_CONFIGS[model_name]
+    return ViT(num_classes=num_classes, num_layers=L, num_heads=Hh, embed_dim=C, patch_shape=(p, p),
+               img_size=img_size, dtype=dtype, device=device)
+
+
+def vit_flops_per_image(model_name: str, img_size: int = 224, num_classes: int = 1000) -> float:
+    """Forward FLOPs per image (2 per MAC): patch GEMM + per layer 4 projections, QK^T, AV and
+    the MLP + head.  Training = 3x."""
+    L, Hh, C, p = MODEL_CONFIGS[model_name]
+    n = (img_size // p) ** 2 + 1
+    per_layer = 2 * n * C * 3 * C + 2 * n * n * C * 2 + 2 * n * C * C + 2 * n * C * 4 * C * 2
+    return float(2 * (n - 1) * p * p * 3 * C + L * per_layer + 2 * C * num_classes)

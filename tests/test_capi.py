@@ -1,0 +1,117 @@
+"""CPU tests of the C ABI boundary: the in-tree library loads, exports every function
+include/sae_attn.h declares, agrees on the descriptor layout, and rejects bad descriptors
+before touching the GPU (validation runs on the host)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sae_attn.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sae_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import sae_vision_amd
+    lib = sae_vision_amd.load_library()
+    names = header_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+    nm = subprocess.run(["nm", "-D", "--defined-only", sae_vision_amd._lib.LIB_PATH], capture_output=True,
+                        text=True).stdout
+    exported = set(re.findall(r" T (sae_\w+)", nm))
+    assert set(names) <= exported, set(names) - exported
+    assert set(sae_vision_amd._lib.EXPORTED_SYMBOLS) == set(names)
+
+
+def test_library_is_gfx950():
+    """The embedded HIP fat binary carries a gfx950 code object (and no other target)."""
+    import sae_vision_amd
+    blob = open(sae_vision_amd._lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_abi_version_and_desc_layout():
+    import sae_vision_amd
+    from sae_vision_amd import _lib as L
+    lib = sae_vision_amd.load_library()
+    assert lib.sae_abi_version() == L.ABI_VERSION
+    # sizeof(sae_attn_desc): 8 x int32 + 24 x int64 + 2 x int32 (natural alignment)
+    assert ctypes.sizeof(L.SaeAttnDesc) == 8 * 4 + 24 * 8 + 2 * 4
+    d = L.SaeAttnDesc()
+    lib.sae_attn_desc_init(ctypes.byref(d), 2, 6, 197, 197, 64, L.SAE_DTYPE_BF16, 0.125)
+    assert list(d.q_stride) == [197 * 6 * 64, 6 * 64, 64]
+    assert list(d.dv_stride) == [197 * 6 * 64, 6 * 64, 64]
+    assert d.scale == pytest.approx(0.125)
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("head_dim", 256, "head_dim 256"),
+    ("dtype", 7, "dtype 7"),
+    ("seq_k", 0, ">= 1"),
+    ("flags", 8, "unknown flags"),
+])
+def test_validation_errors(field, value, msg):
+    import sae_vision_amd
+    from sae_vision_amd import _lib as L
+    lib = sae_vision_amd.load_library()
+    d = L.SaeAttnDesc()
+    lib.sae_attn_desc_init(ctypes.byref(d), 1, 1, 4, 4, 64, L.SAE_DTYPE_F32, 1.0)
+    setattr(d, field, value)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.sae_attn_fwd(None, ctypes.byref(d), dummy, dummy, dummy, None, None, dummy, None)
+    assert rc in (L.SAE_EINVAL, L.SAE_EUNSUPPORTED)
+    assert msg in lib.sae_last_error().decode()
+
+
+def test_relpos_grid_validation():
+    import sae_vision_amd
+    from sae_vision_amd import _lib as L
+    lib = sae_vision_amd.load_library()
+    d = L.SaeAttnDesc()
+    lib.sae_attn_desc_init(ctypes.byref(d), 1, 1, 49, 49, 64, L.SAE_DTYPE_F32, 1.0)
+    d.flags, d.rel_h, d.rel_w = L.SAE_FLAG_RELPOS, 7, 6
+    dummy = ctypes.c_void_p(16)
+    rc = lib.sae_attn_fwd(None, ctypes.byref(d), dummy, dummy, dummy, dummy, dummy, dummy, None)
+    assert rc == L.SAE_EINVAL and "does not match seq_k" in lib.sae_last_error().decode()
+
+
+def test_talking_heads_envelope():
+    import sae_vision_amd
+    from sae_vision_amd import _lib as L
+    lib = sae_vision_amd.load_library()
+    d = L.SaeAttnDesc()
+    lib.sae_attn_desc_init(ctypes.byref(d), 1, 12, 8, 8, 64, L.SAE_DTYPE_F32, 1.0)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.sae_th_attn_fwd(None, ctypes.byref(d), dummy, dummy, dummy, dummy, dummy, dummy, dummy)
+    assert rc == L.SAE_EUNSUPPORTED and "heads <= 8" in lib.sae_last_error().decode()
+
+
+def test_product_path_refuses_cpu_tensors():
+    """No CPU fallback: the ops raise instead of computing on the host."""
+    import torch
+    import sae_vision_amd.ops as ops
+    q = torch.zeros(1, 4, 1, 64)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        ops.attention(q, q, q)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from sae_vision_amd import _lib as L
+    old = L._lib
+    try:
+        L._lib = None
+        with pytest.raises(ImportError, match="no CPU fallback"):
+            L.load(str(tmp_path / "nope.so"))
+    finally:
+        L._lib = old
