@@ -11,11 +11,14 @@
 // P^T feeds O^T = V^T P^T straight from the accumulator registers, V^T read with
 // ds_read_b64_tr_b16.
 //
-// Backward = delta pre-pass + two deterministic passes (no HBM atomics):
-//   attn_bwd_dkdv: key on the lane; a workgroup owns 128 keys and sweeps all query tiles,
-//                  S = Q K^T, dP = dO V^T, dV^T += dO^T P, dK^T += Q^T dS.
-//   attn_bwd_dq  : query on the lane; S^T, dP^T recomputed, dQ^T += K^T dS^T (+ the BoTNet
+// Backward = two deterministic passes (no HBM atomics), in this order:
+//   attn_bwd_dq  : query on the lane; delta = rowsum(dO o O) from the fragments in registers
+//                  (published for the next pass), S^T and dP^T recomputed with -lse/scale and
+//                  -delta as the initial accumulators, dQ^T += K^T dS^T (+ the BoTNet
 //                  relative-logit gradient reduced in LDS).
+//   attn_bwd_dkdv: key on the lane; a workgroup owns 128 keys and sweeps all query tiles,
+//                  S = Q K^T, dP = dO V^T (same accumulator init), dV^T += dO^T P,
+//                  dK^T += Q^T dS.
 #pragma once
 #include "common.h"
 
@@ -64,7 +67,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float* ldsB = reinterpret_cast<float*>(smem + 2 * I::bytes(kBK));   // REL: [4][32][RW]
 
   const int nqb = (a.Nq + kBQ - 1) / kBQ;
-  int bid = blockIdx.x;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb;
   bid /= nqb;
   const int hh = bid % a.H;
@@ -191,38 +194,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// ====================================================================== backward: delta
-// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]  (fp32).  One thread per (b, q, h) row.
-template <typename T>
-__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
-  const long long n = (long long)a.B * a.Nq * a.H;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int hh = (int)(i % a.H);
-  const long long t = i / a.H;
-  const int q = (int)(t % a.Nq);
-  const int b = (int)(t / a.Nq);
-  const T* O = reinterpret_cast<const T*>(a.o) + b * a.os[0] + (long long)q * a.os[1] + hh * a.os[2];
-  const T* G = reinterpret_cast<const T*>(a.dout) + b * a.dos[0] + (long long)q * a.dos[1] + hh * a.dos[2];
-  float acc = 0.f;
-  for (int d = 0; d < a.D; ++d) acc += (float)O[d] * (float)G[d];
-  a.delta[((size_t)b * a.H + hh) * a.Nq + q] = acc;
-}
-
 // ===================================================================== backward: dK, dV
 template <typename T, int DP, bool VEC, bool REL>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
   using M = MF<T>;
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsQ = smem;
   char* ldsG = smem + I::bytes(kBQT);
-  float* ldsL = reinterpret_cast<float*>(smem + 2 * I::bytes(kBQT));   // lse * log2e  [64]
-  float* ldsD = ldsL + kBQT;                                          // delta        [64]
+  float* ldsL = reinterpret_cast<float*>(smem + 2 * I::bytes(kBQT));   // -lse / scale [64]
+  float* ldsD = ldsL + kBQT;                                          // -delta       [64]
   float* ldsB = ldsD + kBQT;                                          // REL: [64][RW]
 
   const int nkb = (a.Nk + kBKV - 1) / kBKV;
-  int bid = blockIdx.x;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kb = bid % nkb;
   bid /= nkb;
   const int hh = bid % a.H;
@@ -270,8 +255,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     gst.write(ldsG, tid);
     if (tid < kBQT) {
       const int qq = qt * kBQT + tid;
-      ldsL[tid] = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
-      ldsD[tid] = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+      ldsL[tid] = qq < a.Nq ? -a.lse[rowoff + qq] / a.scale : -kInf;
+      ldsD[tid] = qq < a.Nq ? -a.delta[rowoff + qq] : 0.f;
     }
     if constexpr (REL) {
       for (int i = tid; i < kBQT * (RW - 1); i += 256) {
@@ -289,23 +274,36 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
       qst.load(Q, (qt + 1) * kBQT, a.Nq, a.qs[1], a.D, tid);
       gst.load(G, (qt + 1) * kBQT, a.Nq, a.dos[1], a.D, tid);
     }
-#pragma unroll
+#pragma unroll 1
     for (int u = 0; u < 2; ++u) {
-      f32x16 sp = zero16(), dp = zero16();
+      // row constants as the initial accumulators: S - lse/scale and dP - delta
+      f32x16 sp, dp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sp[4 * g + j] = l4[j];
+          dp[4 * g + j] = d4[j];
+        }
+      }
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         sp = M::mma(I::rowfrag(ldsQ, 32 * u + r32, s, h), kf[s], sp);
         dp = M::mma(I::rowfrag(ldsG, 32 * u + r32, s, h), vf[s], dp);
       }
-      // sp: S[q = 32u + row_of(r,h)][key = lane]
+      // sp: S[q = 32u + row_of(r,h)][key = lane] - lse/scale; dp: dP - delta
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int ql = 32 * u + row_of(r, h);
-        float x = sp[r] * sl2 - ldsL[ql];
-        if constexpr (REL) x += ldsB[ql * RW + kx] + ldsB[ql * RW + a.rel_h + ky];
+        float x = sp[r] * sl2;
+        if constexpr (REL) {
+          const int ql = 32 * u + row_of(r, h);
+          x += ldsB[ql * RW + kx] + ldsB[ql * RW + a.rel_h + ky];
+        }
         const float p = ex2(x);
         sp[r] = p;
-        dp[r] = p * (dp[r] - ldsD[ql]);
+        dp[r] = p * dp[r];
       }
 #pragma unroll
       for (int s2 = 0; s2 < NP; ++s2) {
@@ -338,7 +336,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
 
 // ========================================================================= backward: dQ
 template <typename T, int DP, bool VEC, bool REL>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
   using M = MF<T>;
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -348,7 +346,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   // REL: dbias accumulators [4][32][RW] follow the bias tables
 
   const int nqb = (a.Nq + kBQ - 1) / kBQ;
-  int bid = blockIdx.x;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb;
   bid /= nqb;
   const int hh = bid % a.H;
@@ -373,9 +371,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     gf[s] = gfrag<T, VEC>(G, q, a.Nq, a.dos[1], a.D, s, h);
   }
   const bool qok = q < a.Nq;
-  const float lse2 = qok ? a.lse[rowoff + q] * kLog2e : kInf;
-  const float dlt = qok ? a.delta[rowoff + q] : 0.f;
-
+  // delta = rowsum(dO * O), from the dO fragments already in registers (this pass runs first
+  // and publishes delta for the dK/dV pass)
+  float dlt;
+  {
+    const T* O = reinterpret_cast<const T*>(a.o) + b * a.os[0] + hh * a.os[2];
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const typename M::frag of = gfrag<T, VEC>(O, q, a.Nq, a.os[1], a.D, s, h);
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)gf[s][j];
+      } else {
+        part += of * gf[s];
+      }
+    }
+    dlt = part + __shfl_xor(part, 32);
+    if (qok && h == 0) a.delta[rowoff + q] = dlt;
+  }
+  const float lsc = qok ? -a.lse[rowoff + q] / a.scale : -kInf;   // S^T init: - lse / scale
   const int RW = a.rel_h + a.rel_w + 1;
   float* wb = ldsB + w * 32 * RW;
   float* wdb = ldsB + 4 * 32 * RW + w * 32 * RW;
@@ -411,19 +426,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
       vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
     }
-#pragma unroll
+#pragma unroll 1
     for (int u = 0; u < 2; ++u) {
-      f32x16 sp = zero16(), dp = zero16();
+      f32x16 sp, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sp[r] = lsc;
+        dp[r] = -dlt;
+      }
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         sp = M::mma(I::rowfrag(ldsK, 32 * u + r32, s, h), qf[s], sp);
         dp = M::mma(I::rowfrag(ldsV, 32 * u + r32, s, h), gf[s], dp);
       }
-      // sp: S^T[key = kt*64 + 32u + row_of(r,h)][q = lane]
+      // sp: S^T[key = kt*64 + 32u + row_of(r,h)][q = lane] - lse/scale; dp: dP^T - delta
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kt * kBK + 32 * u + row_of(r, h);
-        float x = sp[r] * sl2 - lse2;
+        float x = sp[r] * sl2;
         int kx = 0, ky = 0;
         if constexpr (REL) {
           const int kk = min(key, a.Nk - 1);
@@ -432,7 +452,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
           x += wb[r32 * RW + kx] + wb[r32 * RW + a.rel_h + ky];
         }
         const float p = key < a.Nk ? ex2(x) : 0.f;
-        const float ds = p * (dp[r] - dlt);
+        const float ds = p * dp[r];
         dp[r] = ds;
         if constexpr (REL) {
           if (key < a.Nk) {

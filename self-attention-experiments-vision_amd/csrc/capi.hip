@@ -126,10 +126,12 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
   static int run(hipStream_t st, const AttnArgs& a) {
-    {
-      const long long n = (long long)a.B * a.Nq * a.H;
-      hipLaunchKernelGGL((attn_bwd_delta_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
-      int rc = check_launch("attn_bwd_delta");
+    {  // dQ (+ delta) first: it publishes delta for the dK/dV pass
+      const int nqb = (a.Nq + kBQ - 1) / kBQ;
+      const long long grid = (long long)nqb * a.H * a.B;
+      size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 8 * rel_lds_floats(a) * sizeof(float) : 0);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+      int rc = check_launch("attn_bwd_dq");
       if (rc) return rc;
     }
     {
@@ -138,15 +140,7 @@ template <typename T, int DP, bool VEC, bool REL> struct BwdL {
       size_t lds = 2 * Img<T, DP>::bytes(kBQT) + 2 * kBQT * sizeof(float) +
                    (REL ? (size_t)kBQT * (a.rel_h + a.rel_w + 1) * sizeof(float) : 0);
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
-      int rc = check_launch("attn_bwd_dkdv");
-      if (rc) return rc;
-    }
-    {
-      const int nqb = (a.Nq + kBQ - 1) / kBQ;
-      const long long grid = (long long)nqb * a.H * a.B;
-      size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 8 * rel_lds_floats(a) * sizeof(float) : 0);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
-      return check_launch("attn_bwd_dq");
+      return check_launch("attn_bwd_dkdv");
     }
   }
 };

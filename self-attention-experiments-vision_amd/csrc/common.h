@@ -215,6 +215,15 @@ __device__ __forceinline__ void store4(T* rowp, int d0, int D, float a, float b,
   }
 }
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): hardware block `bid` of a
+// G-block grid runs on XCD bid % 8; returning logical ids so that consecutive logical blocks
+// (which share K/V or Q/dO of one (batch, head)) land on the same XCD and its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int G) {
+  const int x = bid & 7, j = bid >> 3;
+  const int q = G >> 3, r = G & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
 // exact integer key -> (row, col) split for key < 4096, width <= 64: (key * magic) >> 20
 __host__ __device__ inline int div_magic(int w) { return (int)((1u << 20) / (unsigned)w + 1u); }
 

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the fused attention kernels (fwd, bwd) at the BASELINE shapes.
+
+    python tools/attn_bench.py [--iters 50] [--shapes deit_s,vitb384,...] [--dtype bf16]
+
+Times each C-ABI call with HIP events on the launch stream (median over iterations) and
+prints TFLOP/s and GB/s with the algorithmic counts of SURVEY §8d.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SHAPES = {  # name: (B, Nq, Nk, H, D)
+    "deit_s": (128, 197, 197, 6, 64),
+    "deit_s_b256": (256, 197, 197, 6, 64),
+    "vitb384": (64, 577, 577, 12, 64),
+    "cait_s24": (256, 196, 196, 8, 48),
+    "cait_ca": (256, 1, 197, 8, 48),
+    "bot14": (256, 196, 196, 4, 128),
+    "bot7": (256, 49, 49, 4, 128),
+    "cvt1": (64, 3136, 784, 1, 64),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--shapes", default="deit_s,vitb384,cait_s24,cait_ca,bot14,bot7")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    import torch
+    import sae_vision_amd.ops as ops
+
+    dev = torch.device("cuda:0")
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    elt = 2 if args.dtype == "bf16" else 4
+    results = {}
+    for name in args.shapes.split(","):
+        B, Nq, Nk, H, D = SHAPES[name]
+        g = torch.Generator(device=dev).manual_seed(0)
+        q = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
+        k = torch.randn(B, Nk, H, D, device=dev, generator=g).to(dt)
+        v = torch.randn(B, Nk, H, D, device=dev, generator=g).to(dt)
+        do = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        sc = 1.0 / math.sqrt(D)
+        o, lse = ops._fwd(q, k, v, sc)
+        ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+        torch.cuda.synchronize()
+        tf, tb = [], []
+        for _ in range(args.iters):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            o, lse = ops._fwd(q, k, v, sc)
+            e[1].record()
+            ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+            e[2].record()
+            torch.cuda.synchronize()
+            tf.append(e[0].elapsed_time(e[1]))
+            tb.append(e[1].elapsed_time(e[2]))
+        tf.sort()
+        tb.sort()
+        mf, mb = tf[len(tf) // 2] / 1e3, tb[len(tb) // 2] / 1e3
+        ff, fb = 4.0 * B * H * Nq * Nk * D, 8.0 * B * H * Nq * Nk * D
+        bf = elt * B * H * D * (2 * Nq + 2 * Nk) + 4 * B * H * Nq
+        bb = elt * B * H * D * (4 * Nq + 4 * Nk) + 8 * B * H * Nq
+        r = {"fwd_us": round(mf * 1e6, 1), "bwd_us": round(mb * 1e6, 1),
+             "fwd_tflops": round(ff / mf / 1e12, 1), "bwd_tflops": round(fb / mb / 1e12, 1),
+             "fwdbwd_tflops": round((ff + fb) / (mf + mb) / 1e12, 1),
+             "fwd_gbs": round(bf / mf / 1e9), "bwd_gbs": round(bb / mb / 1e9)}
+        results[name] = r
+        print(f"{name:12s} B={B:4d} Nq={Nq:5d} Nk={Nk:5d} H={H:3d} D={D:4d} | fwd {r['fwd_us']:8.1f} us "
+              f"{r['fwd_tflops']:7.1f} TF {r['fwd_gbs']:6d} GB/s | bwd {r['bwd_us']:8.1f} us {r['bwd_tflops']:7.1f} TF "
+              f"{r['bwd_gbs']:6d} GB/s | fwd+bwd {r['fwdbwd_tflops']:7.1f} TF", flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
