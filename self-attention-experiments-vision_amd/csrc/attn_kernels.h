@@ -51,20 +51,105 @@ constexpr int kBK = 64;    // keys per staged K/V tile
 constexpr int kBKV = 128;  // keys per dkdv workgroup (4 waves x 32)
 constexpr int kBQT = 64;   // query rows per staged tile in dkdv
 
+// K/V (or Q/dO) tiles are double-buffered (one barrier per tile) except fp32 at head_dim 128,
+// whose tiles are too large for two buffers plus the BoTNet tables in 160 KiB of LDS.
+template <typename T, int DP> constexpr int nbuf() { return (sizeof(T) == 4 && DP == 128) ? 1 : 2; }
+
 template <typename T, int DP, bool REL>
 constexpr int fwd_lds_bytes_static() {
   return 2 * Img<T, DP>::bytes(kBK);
 }
 
 // ================================================================================ forward
+// Lazy rescale (cdna_hip_programming.md T13): the running max m is only moved when some row's
+// tile max exceeds it by more than THR (log2 units), so P <= 2^THR.  bf16: THR = 8 (P is fed to
+// the MFMA in bf16, whose relative precision does not depend on magnitude); f32: THR = 0 (exact
+// textbook online softmax).  The decision is wave-uniform and taken before any P of the tile is
+// exponentiated (T13 safe order).
+template <typename T> struct LazyThr { static constexpr float v = sizeof(T) == 2 ? 8.f : 0.f; };
+
+template <typename T, int DP, bool REL, bool MASK>
+__device__ __forceinline__ void fwd_tile(const char* ldsK, const char* ldsV, const typename MF<T>::frag* qf,
+                                         f32x16* acco, float& m, float& l, int key0, int Nk, float sl2,
+                                         const float* wbrow, int rel_h, int rel_w, int rel_magic, int h, int r32,
+                                         int lane) {
+  using M = MF<T>;
+  using I = Img<T, DP>;
+  constexpr int NS = DP / M::KSTEP, NP = 32 / M::KSTEP, NT = DP / 32;
+  // masked tail: the second 32-key half is skipped when it holds no valid key
+  const bool two = !MASK || key0 + 32 < Nk;
+  f32x16 sacc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    sacc[u] = zero16();
+    if (u == 1 && !two) continue;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) sacc[u] = M::mma(I::rowfrag(ldsK, 32 * u + r32, s, h), qf[s], sacc[u]);
+  }
+  // scores: REL -> x = s*sl2 + bias (log2 domain); otherwise keep raw s and fold sl2 into the exp FMA
+  float mx = -kInf;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !two) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = key0 + 32 * u + row_of(r, h);
+      float x = sacc[u][r];
+      if constexpr (REL) {
+        const int kk = min(key, Nk - 1);
+        const int kx = (kk * rel_magic) >> 20;
+        const int ky = kk - kx * rel_w;
+        x = x * sl2 + wbrow[kx] + wbrow[rel_h + ky];
+      }
+      if constexpr (MASK) x = key < Nk ? x : -kInf;
+      sacc[u][r] = x;
+      mx = fmaxf(mx, x);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  if constexpr (!REL) mx *= sl2;                  // scale > 0 (validated)
+  if (!__all(mx - m <= LazyThr<T>::v)) {
+    const float mn = fmaxf(m, mx);
+    const float alpha = ex2(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acco[t][r] *= alpha;
+  }
+  float ls = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !two) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = REL ? ex2(sacc[u][r] - m) : ex2(__builtin_fmaf(sacc[u][r], sl2, -m));
+      sacc[u][r] = p;
+      ls += p;
+    }
+  }
+  l += ls;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !two) continue;
+#pragma unroll
+    for (int s2 = 0; s2 < NP; ++s2) {
+      const typename M::frag pf = acc_frag<T>(sacc[u], s2);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acco[t] = M::mma(I::colfrag(ldsV, 32 * u, s2, 32 * t, lane), pf, acco[t]);
+    }
+  }
+}
+
 template <typename T, int DP, bool VEC, bool REL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DP >= 128 ? 1 : ((DP == 64 && sizeof(T) == 2 && !REL && VEC) ? 3 : 2)) void attn_fwd_kernel(AttnArgs a) {
   using M = MF<T>;
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsK = smem;
-  char* ldsV = smem + I::bytes(kBK);
-  float* ldsB = reinterpret_cast<float*>(smem + 2 * I::bytes(kBK));   // REL: [4][32][RW]
+  // double-buffered K/V tiles: [buf][K | V], one barrier per key tile
+  constexpr int TB = 2 * I::bytes(kBK);
+  float* ldsB = reinterpret_cast<float*>(smem + nbuf<T, DP>() * TB);   // REL: [4][32][RW]
 
   const int nqb = (a.Nq + kBQ - 1) / kBQ;
   int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -74,13 +159,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const int b = bid / a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
   const int q = qb * kBQ + w * 32 + r32;
+  const bool active = qb * kBQ + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nq;
 
   const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
   const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
   const T* V = reinterpret_cast<const T*>(a.v) + b * a.vs[0] + hh * a.vs[2];
 
   constexpr int NS = DP / M::KSTEP;        // k-steps over the head dim
-  constexpr int NP = 32 / M::KSTEP;        // k-steps over a 32-key accumulator
   constexpr int NT = DP / 32;              // 32-wide head-dim tiles of O^T
 
   typename M::frag qf[NS];
@@ -102,6 +187,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       wb[rr * RW + cc] = val * kLog2e;
     }
   }
+  const float* wbrow = ldsB + (w * 32 + r32) * RW;
 
   f32x16 acco[NT];
 #pragma unroll
@@ -109,75 +195,50 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float m = -kInf, l = 0.f;
   const float sl2 = a.scale * kLog2e;
   const int nkt = (a.Nk + kBK - 1) / kBK;
+  const int nfull = a.Nk / kBK;
 
   Stage<T, DP, kBK, VEC> kst, vst;
-  kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
-  vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+  const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+  const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+  if constexpr (VEC) {
+    kst.load_buf(rk, 0, a.ks[1], a.D, tid);
+    vst.load_buf(rv, 0, a.vs[1], a.D, tid);
+  } else {
+    kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
+    vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+  }
 
+  kst.write(smem, tid);
+  vst.write(smem + I::bytes(kBK), tid);
+  __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
+    const char* ldsK = smem + (nbuf<T, DP>() == 2 ? (kt & 1) : 0) * TB;
+    const char* ldsV = ldsK + I::bytes(kBK);
+    const bool more = kt + 1 < nkt;
+    if (more) {                               // next tile global -> registers, in flight during compute
+      if constexpr (VEC) {
+        kst.load_buf(rk, (kt + 1) * kBK, a.ks[1], a.D, tid);
+        vst.load_buf(rv, (kt + 1) * kBK, a.vs[1], a.D, tid);
+      } else {
+        kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
+        vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
+      }
+    }
+    if (active) {                              // waves with no valid query row only stage + sync
+      if (kt < nfull)
+        fwd_tile<T, DP, REL, false>(ldsK, ldsV, qf, acco, m, l, kt * kBK, a.Nk, sl2, wbrow, a.rel_h, a.rel_w,
+                                    a.rel_magic, h, r32, lane);
+      else
+        fwd_tile<T, DP, REL, true>(ldsK, ldsV, qf, acco, m, l, kt * kBK, a.Nk, sl2, wbrow, a.rel_h, a.rel_w,
+                                   a.rel_magic, h, r32, lane);
+    }
+    if (more) {                               // the other buffer was last read before the previous barrier
+      if (nbuf<T, DP>() == 1) __syncthreads();
+      char* nk = smem + (nbuf<T, DP>() == 2 ? ((kt + 1) & 1) : 0) * TB;
+      kst.write(nk, tid);
+      vst.write(nk + I::bytes(kBK), tid);
+    }
     __syncthreads();
-    kst.write(ldsK, tid);
-    vst.write(ldsV, tid);
-    __syncthreads();
-    if (kt + 1 < nkt) {
-      kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
-      vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
-    }
-    f32x16 sacc[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      sacc[u] = zero16();
-#pragma unroll
-      for (int s = 0; s < NS; ++s) sacc[u] = M::mma(I::rowfrag(ldsK, 32 * u + r32, s, h), qf[s], sacc[u]);
-    }
-    float mx = -kInf;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * kBK + 32 * u + row_of(r, h);
-        float x = sacc[u][r] * sl2;
-        if constexpr (REL) {
-          const int kk = min(key, a.Nk - 1);
-          const int kx = (kk * a.rel_magic) >> 20;
-          const int ky = kk - kx * a.rel_w;
-          const float* wb = ldsB + (w * 32 + r32) * RW;
-          x += wb[kx] + wb[a.rel_h + ky];
-        }
-        x = key < a.Nk ? x : -kInf;
-        sacc[u][r] = x;
-        mx = fmaxf(mx, x);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float mn = fmaxf(m, mx);
-    const float alpha = ex2(m - mn);
-    m = mn;
-    float ls = 0.f;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = ex2(sacc[u][r] - mn);
-        sacc[u][r] = p;
-        ls += p;
-      }
-    }
-    l = l * alpha + ls;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acco[t][r] *= alpha;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int s2 = 0; s2 < NP; ++s2) {
-        const typename M::frag pf = acc_frag<T>(sacc[u], s2);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acco[t] = M::mma(I::colfrag(ldsV, 32 * u, s2, 32 * t, lane), pf, acco[t]);
-      }
-    }
   }
 
   l += __shfl_xor(l, 32);
@@ -200,11 +261,9 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   using M = MF<T>;
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsQ = smem;
-  char* ldsG = smem + I::bytes(kBQT);
-  float* ldsL = reinterpret_cast<float*>(smem + 2 * I::bytes(kBQT));   // -lse / scale [64]
-  float* ldsD = ldsL + kBQT;                                          // -delta       [64]
-  float* ldsB = ldsD + kBQT;                                          // REL: [64][RW]
+  // double-buffered query tile: [buf][Q img | dO img | -lse/scale [64] | -delta [64] | REL bias [64][RW]]
+  const int RW = a.rel_h + a.rel_w + 1;
+  const int TB = 2 * I::bytes(kBQT) + 2 * kBQT * 4 + (REL ? kBQT * RW * 4 : 0);
 
   const int nkb = (a.Nk + kBKV - 1) / kBKV;
   int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -214,6 +273,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   const int b = bid / a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
   const int key = kb * kBKV + w * 32 + r32;
+  const bool active = kb * kBKV + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nk;
 
   const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
   const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
@@ -236,7 +296,6 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   for (int t = 0; t < NT; ++t) { adk[t] = zero16(); adv[t] = zero16(); }
 
   const float sl2 = a.scale * kLog2e;
-  const int RW = a.rel_h + a.rel_w + 1;
   int kx = 0, ky = 0;
   if constexpr (REL) {
     const int kk = min(key, a.Nk - 1);
@@ -246,19 +305,29 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   const int nqt = (a.Nq + kBQT - 1) / kBQT;
 
   Stage<T, DP, kBQT, VEC> qst, gst;
-  qst.load(Q, 0, a.Nq, a.qs[1], a.D, tid);
-  gst.load(G, 0, a.Nq, a.dos[1], a.D, tid);
+  const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
+  const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
+  if constexpr (VEC) {
+    qst.load_buf(rq, 0, a.qs[1], a.D, tid);
+    gst.load_buf(rg, 0, a.dos[1], a.D, tid);
+  } else {
+    qst.load(Q, 0, a.Nq, a.qs[1], a.D, tid);
+    gst.load(G, 0, a.Nq, a.dos[1], a.D, tid);
+  }
 
-  for (int qt = 0; qt < nqt; ++qt) {
-    __syncthreads();
-    qst.write(ldsQ, tid);
-    gst.write(ldsG, tid);
+  // writes the staged Q / dO registers and this tile's row constants into buffer `buf`
+  auto put = [&](char* buf, int qt) {
+    qst.write(buf, tid);
+    gst.write(buf + I::bytes(kBQT), tid);
+    float* L = reinterpret_cast<float*>(buf + 2 * I::bytes(kBQT));
+    float* Dl = L + kBQT;
     if (tid < kBQT) {
       const int qq = qt * kBQT + tid;
-      ldsL[tid] = qq < a.Nq ? -a.lse[rowoff + qq] / a.scale : -kInf;
-      ldsD[tid] = qq < a.Nq ? -a.delta[rowoff + qq] : 0.f;
+      L[tid] = qq < a.Nq ? -a.lse[rowoff + qq] / a.scale : -kInf;
+      Dl[tid] = qq < a.Nq ? -a.delta[rowoff + qq] : 0.f;
     }
     if constexpr (REL) {
+      float* Bb = Dl + kBQT;
       for (int i = tid; i < kBQT * (RW - 1); i += 256) {
         const int rr = i / (RW - 1), cc = i % (RW - 1);
         const int qq = qt * kBQT + rr;
@@ -266,16 +335,32 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         if (qq < a.Nq)
           val = cc < a.rel_h ? a.bias_h[(rowoff + qq) * a.rel_h + cc]
                              : a.bias_w[(rowoff + qq) * a.rel_w + (cc - a.rel_h)];
-        ldsB[rr * RW + cc] = val * kLog2e;
+        Bb[rr * RW + cc] = val * kLog2e;
       }
     }
-    __syncthreads();
-    if (qt + 1 < nqt) {
-      qst.load(Q, (qt + 1) * kBQT, a.Nq, a.qs[1], a.D, tid);
-      gst.load(G, (qt + 1) * kBQT, a.Nq, a.dos[1], a.D, tid);
+  };
+  put(smem, 0);
+  __syncthreads();
+
+  for (int qt = 0; qt < nqt; ++qt) {
+    const char* ldsQ = smem + (nbuf<T, DP>() == 2 ? (qt & 1) : 0) * TB;
+    const char* ldsG = ldsQ + I::bytes(kBQT);
+    const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * I::bytes(kBQT));
+    const float* ldsD = ldsL + kBQT;
+    const float* ldsB = ldsD + kBQT;
+    const bool more = qt + 1 < nqt;
+    if (more) {
+      if constexpr (VEC) {
+        qst.load_buf(rq, (qt + 1) * kBQT, a.qs[1], a.D, tid);
+        gst.load_buf(rg, (qt + 1) * kBQT, a.dos[1], a.D, tid);
+      } else {
+        qst.load(Q, (qt + 1) * kBQT, a.Nq, a.qs[1], a.D, tid);
+        gst.load(G, (qt + 1) * kBQT, a.Nq, a.dos[1], a.D, tid);
+      }
     }
+    const int nu = !active ? 0 : (qt * kBQT + 32 < a.Nq ? 2 : 1);   // skip padding halves / idle waves
 #pragma unroll 1
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < nu; ++u) {
       // row constants as the initial accumulators: S - lse/scale and dP - delta
       f32x16 sp, dp;
 #pragma unroll
@@ -316,6 +401,11 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         }
       }
     }
+    if (more) {
+      if (nbuf<T, DP>() == 1) __syncthreads();
+      put(smem + (nbuf<T, DP>() == 2 ? ((qt + 1) & 1) : 0) * TB, qt + 1);
+    }
+    __syncthreads();
   }
 
   if (key < a.Nk) {
@@ -340,9 +430,8 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   using M = MF<T>;
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsK = smem;
-  char* ldsV = smem + I::bytes(kBK);
-  float* ldsB = reinterpret_cast<float*>(smem + 2 * I::bytes(kBK));   // REL: bias [4][32][RW]
+  constexpr int TB = 2 * I::bytes(kBK);                              // [buf][K | V]
+  float* ldsB = reinterpret_cast<float*>(smem + nbuf<T, DP>() * TB);  // REL: bias [4][32][RW]
   // REL: dbias accumulators [4][32][RW] follow the bias tables
 
   const int nqb = (a.Nq + kBQ - 1) / kBQ;
@@ -353,6 +442,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   const int b = bid / a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
   const int q = qb * kBQ + w * 32 + r32;
+  const bool active = qb * kBQ + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nq;
 
   const T* Q = reinterpret_cast<const T*>(a.q) + b * a.qs[0] + hh * a.qs[2];
   const T* K = reinterpret_cast<const T*>(a.k) + b * a.ks[0] + hh * a.ks[2];
@@ -414,20 +504,36 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   const int nkt = (a.Nk + kBK - 1) / kBK;
 
   Stage<T, DP, kBK, VEC> kst, vst;
-  kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
-  vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+  const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+  const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+  if constexpr (VEC) {
+    kst.load_buf(rk, 0, a.ks[1], a.D, tid);
+    vst.load_buf(rv, 0, a.vs[1], a.D, tid);
+  } else {
+    kst.load(K, 0, a.Nk, a.ks[1], a.D, tid);
+    vst.load(V, 0, a.Nk, a.vs[1], a.D, tid);
+  }
 
+  kst.write(smem, tid);
+  vst.write(smem + I::bytes(kBK), tid);
+  __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
-    kst.write(ldsK, tid);
-    vst.write(ldsV, tid);
-    __syncthreads();
-    if (kt + 1 < nkt) {
-      kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
-      vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
+    const char* ldsK = smem + (nbuf<T, DP>() == 2 ? (kt & 1) : 0) * TB;
+    const char* ldsV = ldsK + I::bytes(kBK);
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      if constexpr (VEC) {
+        kst.load_buf(rk, (kt + 1) * kBK, a.ks[1], a.D, tid);
+        vst.load_buf(rv, (kt + 1) * kBK, a.vs[1], a.D, tid);
+      } else {
+        kst.load(K, (kt + 1) * kBK, a.Nk, a.ks[1], a.D, tid);
+        vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
+      }
     }
+    const int nu = !active ? 0 : (kt * kBK + 32 < a.Nk ? 2 : 1);   // skip padding halves / idle waves
+    const bool tail = (kt + 1) * kBK > a.Nk;           // only the last tile needs the key mask
 #pragma unroll 1
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < nu; ++u) {
       f32x16 sp, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -451,7 +557,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
           ky = kk - kx * a.rel_w;
           x += wb[r32 * RW + kx] + wb[r32 * RW + a.rel_h + ky];
         }
-        const float p = key < a.Nk ? ex2(x) : 0.f;
+        const float p = (!tail || key < a.Nk) ? ex2(x) : 0.f;
         const float ds = p * dp[r];
         dp[r] = ds;
         if constexpr (REL) {
@@ -468,6 +574,13 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
         for (int t = 0; t < NT; ++t) adq[t] = M::mma(I::colfrag(ldsK, 32 * u, s2, 32 * t, lane), sf, adq[t]);
       }
     }
+    if (more) {
+      if (nbuf<T, DP>() == 1) __syncthreads();
+      char* nk = smem + (nbuf<T, DP>() == 2 ? ((kt + 1) & 1) : 0) * TB;
+      kst.write(nk, tid);
+      vst.write(nk + I::bytes(kBK), tid);
+    }
+    __syncthreads();
   }
 
   if (qok) {

@@ -63,6 +63,21 @@ int validate(const sae_attn_desc* d, bool bwd) {
       return fail(SAE_EUNSUPPORTED, "relpos grid %dx%d exceeds 64x64", d->rel_h, d->rel_w);
   }
   if (d->seq_q > (1 << 24) || d->seq_k > (1 << 24)) return fail(SAE_EUNSUPPORTED, "sequence too long");
+  if (!(d->scale > 0.f)) return fail(SAE_EINVAL, "scale must be > 0 (got %g)", (double)d->scale);
+  {  // per-(batch, head) row ranges are addressed through 32-bit buffer descriptors
+    const int es = d->dtype == SAE_DTYPE_BF16 ? 2 : 4;
+    const int64_t* st[8] = {d->q_stride, d->k_stride, d->v_stride, d->o_stride,
+                            d->do_stride, d->dq_stride, d->dk_stride, d->dv_stride};
+    const char* nm[8] = {"q", "k", "v", "o", "dout", "dq", "dk", "dv"};
+    for (int i = 0; i < (bwd ? 8 : 4); ++i) {
+      const int64_t n = (i == 1 || i == 2 || i == 6 || i == 7) ? d->seq_k : d->seq_q;
+      if (st[i][1] < d->head_dim)
+        return fail(SAE_EINVAL, "%s token stride %lld < head_dim %d", nm[i], (long long)st[i][1], d->head_dim);
+      if (n * st[i][1] * es >= ((int64_t)1 << 31))
+        return fail(SAE_EUNSUPPORTED, "%s: %lld tokens x stride %lld exceed 32-bit row addressing", nm[i],
+                    (long long)n, (long long)st[i][1]);
+    }
+  }
   (void)bwd;
   return SAE_OK;
 }
@@ -111,6 +126,16 @@ int dispatch(int dtype, int dp, bool vec, bool rel, Args&&... args) {
   return fail(SAE_EUNSUPPORTED, "no kernel instance for dtype %d dp %d", dtype, dp);
 }
 
+// Kernels asking for more than 64 KiB of dynamic LDS raise their limit once (up to the 160 KiB
+// of a gfx950 CU); failure is reported, never silently ignored.
+int lds_attr(const void* fn, size_t bytes) {
+  if (bytes > 160 * 1024) return fail(SAE_EUNSUPPORTED, "kernel needs %zu bytes of LDS (> 160 KiB)", bytes);
+  if (bytes <= 64 * 1024) return SAE_OK;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return fail(SAE_EHIP, "hipFuncSetAttribute(%zu B LDS): %s", bytes, hipGetErrorString(e));
+  return SAE_OK;
+}
+
 int rel_lds_floats(const AttnArgs& a) { return a.rel_h ? 32 * (a.rel_h + a.rel_w + 1) : 0; }
 
 template <typename T, int DP, bool VEC, bool REL> struct FwdL {
@@ -118,7 +143,8 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
     const int nqb = (a.Nq + kBQ - 1) / kBQ;
     const long long grid = (long long)nqb * a.H * a.B;
     if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-    size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 4 * rel_lds_floats(a) * sizeof(float) : 0);
+    size_t lds = nbuf<T, DP>() * 2 * Img<T, DP>::bytes(kBK) + (REL ? 4 * rel_lds_floats(a) * sizeof(float) : 0);
+    if (int rc = lds_attr((const void*)attn_fwd_kernel<T, DP, VEC, REL>, lds)) return rc;
     hipLaunchKernelGGL((attn_fwd_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
     return check_launch("attn_fwd");
   }
@@ -129,7 +155,8 @@ template <typename T, int DP, bool VEC, bool REL> struct BwdL {
     {  // dQ (+ delta) first: it publishes delta for the dK/dV pass
       const int nqb = (a.Nq + kBQ - 1) / kBQ;
       const long long grid = (long long)nqb * a.H * a.B;
-      size_t lds = 2 * Img<T, DP>::bytes(kBK) + (REL ? 8 * rel_lds_floats(a) * sizeof(float) : 0);
+      size_t lds = nbuf<T, DP>() * 2 * Img<T, DP>::bytes(kBK) + (REL ? 8 * rel_lds_floats(a) * sizeof(float) : 0);
+      if (int rc = lds_attr((const void*)attn_bwd_dq_kernel<T, DP, VEC, REL>, lds)) return rc;
       hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
       int rc = check_launch("attn_bwd_dq");
       if (rc) return rc;
@@ -137,8 +164,9 @@ template <typename T, int DP, bool VEC, bool REL> struct BwdL {
     {
       const int nkb = (a.Nk + kBKV - 1) / kBKV;
       const long long grid = (long long)nkb * a.H * a.B;
-      size_t lds = 2 * Img<T, DP>::bytes(kBQT) + 2 * kBQT * sizeof(float) +
-                   (REL ? (size_t)kBQT * (a.rel_h + a.rel_w + 1) * sizeof(float) : 0);
+      size_t lds = nbuf<T, DP>() * (2 * Img<T, DP>::bytes(kBQT) + 2 * kBQT * sizeof(float) +
+                        (REL ? (size_t)kBQT * (a.rel_h + a.rel_w + 1) * sizeof(float) : 0));
+      if (int rc = lds_attr((const void*)attn_bwd_dkdv_kernel<T, DP, VEC, REL>, lds)) return rc;
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, DP, VEC, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
       return check_launch("attn_bwd_dkdv");
     }

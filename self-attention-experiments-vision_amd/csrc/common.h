@@ -152,6 +152,18 @@ template <typename T, int DP, int ROWS, bool VEC> struct Stage {
       }
     }
   }
+  // VEC path through a buffer descriptor whose range ends at row `nrows`: rows past the end and
+  // columns >= D read as zero from the hardware range check -- no branches (T8/T20).
+  __device__ __forceinline__ void load_buf(__amdgpu_buffer_rsrc_t rsrc, int row0, long long rs, int D, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 256 * i;
+      const int r = id / CPR, c = id % CPR;
+      unsigned off = (unsigned)(((long long)(row0 + r) * rs + c * EPC) * (long long)sizeof(T));
+      off = (c * EPC < D && id < ROWS * CPR) ? off : 0x80000000u;
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+    }
+  }
   __device__ __forceinline__ void write(char* lds, int tid) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -170,6 +182,13 @@ template <typename T, int DP, int ROWS, bool VEC> struct Stage {
     }
   }
 };
+
+// Buffer descriptor over rows [0, nrows) of a token-major tensor (row stride rs elements),
+// built from wave-uniform values only.
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const T* base, int nrows, long long rs) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long long)nrows * rs * sizeof(T)), 0x00020000);
+}
 
 // Operand fragment read straight from global memory: row `row` of a token-major tensor,
 // elements d = KSTEP*s + KH*h + j.

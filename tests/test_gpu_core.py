@@ -115,20 +115,34 @@ def test_deterministic(dev):
         assert torch.equal(a, b)
 
 
-def test_softmax_spike(dev):
-    """Forces the online-softmax rescale: one key dominates at a late tile (rule 26)."""
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("gain", [0.05, 0.6, 4.0])
+def test_softmax_spike(dev, mode, gain):
+    """Forces the online-softmax max to jump at a late key tile (rule 26): gain 4 jumps far past
+    the lazy-rescale threshold (rescale branch), gain 0.6 jumps by a few log2 units (bf16: kept
+    below the threshold, P > 1 path), gain 0.05 barely moves it."""
     import torch
     import sae_vision_amd.ops as ops
 
     rng = np.random.default_rng(5)
     B, N, H, D = 1, 300, 2, 64
-    q = rng.standard_normal((B, N, H, D)).astype(np.float32)
-    k = rng.standard_normal((B, N, H, D)).astype(np.float32)
-    v = rng.standard_normal((B, N, H, D)).astype(np.float32)
-    k[0, 250] = q[0, 7] * 4.0          # spike for query 7 in the 4th key tile
-    k[0, 0] = -q[0, 7] * 3.0
-    o = ops.attention(*(torch.tensor(x, device=dev) for x in (q, k, v)))
-    assert rel_err(o.cpu().numpy(), R.attention_core_fwd(q, k, v, "f64")) <= TOL["f32"]
+    q = randn(rng, (B, N, H, D), mode)
+    k = randn(rng, (B, N, H, D), mode) * 0.3
+    v = randn(rng, (B, N, H, D), mode)
+    for qi in (7, 40, 127, 200):
+        k[0, 250 - qi // 2] = q[0, qi] * gain          # spike in a late tile
+        k[0, qi % 64] = -q[0, qi] * gain                 # anti-spike in the first tile
+    if mode == "bf16":
+        k = R.round_bf16(k)
+    td = torch.bfloat16 if mode == "bf16" else torch.float32
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=td, requires_grad=True) for x in (q, k, v))
+    o = ops.attention(tq, tk, tv)
+    do = randn(np.random.default_rng(2), (B, N, H, D), mode)
+    o.backward(torch.tensor(do, device=dev, dtype=td))
+    assert rel_err(o, R.attention_core_fwd(q, k, v, "f64" if mode == "f32" else "bf16")) <= TOL[mode]
+    g = R.attention_core_bwd(q, k, v, do)
+    for n, t in (("dq", tq), ("dk", tk), ("dv", tv)):
+        assert rel_err(t.grad, g[n]) <= TOL[mode], n
 
 
 def test_error_reporting(dev):
