@@ -11,9 +11,10 @@ overlapped with the backward).  W untimed warm-up steps, then exactly K steps br
 barrier + device synchronisation on both sides; the max elapsed time over ranks is used.
 Rank 0 prints ONE JSON line:
   value        = whole-job training images/s (all ranks)
-  roofline     = the fused attention op of this workload (fwd + bwd = 4 launches: attn_fwd,
-                 attn_bwd_delta, attn_bwd_dkdv, attn_bwd_dq), timed live with HIP events on its
-                 launch stream inside the timed region; algorithmic FLOPs/bytes per call
+  roofline     = the fused attention op of this workload (fwd + bwd = 3 launches: attn_fwd,
+                 attn_bwd_dq (+ delta), attn_bwd_dkdv), timed live with HIP events on its launch
+                 stream inside the timed region; algorithmic FLOPs/bytes per call (DESIGN.md §4);
+                 traffic = HBM bytes per call from profiles/pmc_traffic.json (rocprofv3 PMC)
   cpu_baseline = the numpy port (oracle/vit_ref.py) of the same training step on a bounded
                  sample, on this host's cores (rank 0, N=1 only)
   attention_headline = the fused fwd+bwd core alone at ViT-B/16@384 shape (B=64, N=577, H=12,
