@@ -34,7 +34,7 @@ def build(force=False, debug=False, verbose=True):
             print(f"[build] {OUT} is up to date")
         return OUT
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-I", os.path.join(ROOT, "include"),
+           "-Wno-unused-function", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-I", os.path.join(ROOT, "include"),
            os.path.join(SRC, "capi.hip"), "-o", OUT + ".tmp"]
     if debug:
         cmd.insert(3, "-g")

@@ -1,0 +1,340 @@
+// bwd2.h -- lean bf16 attention backward for gfx950 (dQ pass, then dK/dV pass).
+//
+// Same two deterministic passes as attn_bwd_dq_kernel / attn_bwd_dkdv_kernel (attn_kernels.h;
+// the JAX autodiff of models/layers/attentions/attention.py:39-58), rebuilt the way fwd2.h is:
+//   * every per-tile address precomputed once (buffer-descriptor offsets, VGPR + immediate LDS
+//     addresses, tile loop unrolled over the two LDS buffers);
+//   * score accumulators start at zero (a free immediate C operand) and the row constants enter
+//     through the exponent's FMA: p = 2^(s * scale * log2e - lse * log2e), dS = p (dP - delta);
+//   * the dK/dV pass prefetches the per-query row constants with the Q / dO tile (issue early,
+//     write late): no dependent global load inside the loop;
+//   * results leave through a per-wave LDS scratch as whole 16-byte row chunks (wave_store_rows).
+#pragma once
+#include "fwd2.h"
+
+namespace sae {
+
+// ------------------------------------------------------------------------------- dQ pass
+// One wave = 32 query rows (query on the MFMA lane), NW waves share each 64-key K/V tile.
+// delta = rowsum(dO o O) is computed from the fragments in registers and published for the
+// dK/dV pass.  Per 32-key half: S^T = K Q^T, dP^T = V dO^T (row reads of the K / V images),
+// dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T (transposed reads of the K image).
+template <int DP, int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a) {
+  using FF = F2<DP>;
+  constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
+  constexpr int BQ = 32 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (a.Nq + BQ - 1) / BQ;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb;
+  bid /= nqb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * BQ + w * 32 + r32;
+  const bool active = qb * BQ + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nq;
+  const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+  const __bf16* O = reinterpret_cast<const __bf16*>(a.o) + b * a.os[0] + hh * a.os[2];
+  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
+
+  F2Stage<DP, NW> kst, vst;
+  kst.init(tid, a.ks[1], a.D);
+  vst.init(tid, a.vs[1], a.D);
+  const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+  const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+  const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
+  kst.load(rk, 0);
+  vst.load(rv, 0);
+
+  bf16x8 qf[NS], gf[NS];
+  float dlt;
+  {
+    const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
+    const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
+    const __amdgpu_buffer_rsrc_t ro = row_rsrc(O, a.Nq, a.os[1]);
+    const unsigned qo = (unsigned)((long long)q * a.qs[1] * 2);
+    const unsigned go = (unsigned)((long long)q * a.dos[1] * 2);
+    const unsigned oo = (unsigned)((long long)q * a.os[1] * 2);
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      const bool ok = d0 < a.D;
+      qf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, ok ? qo + d0 * 2 : 0x80000000u, 0, 0));
+      gf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rg, ok ? go + d0 * 2 : 0x80000000u, 0, 0));
+      const bf16x8 of = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ro, ok ? oo + d0 * 2 : 0x80000000u, 0, 0));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)gf[s][j];
+    }
+    dlt = xhalf_sum(part);
+  }
+  const bool qok = q < a.Nq;
+  if (qok && h == 0) a.delta[rowoff + q] = dlt;
+  const float lsc2 = qok ? -a.lse[rowoff + q] * kLog2e : -kInf;
+  const float sl2 = a.scale * kLog2e;
+
+  unsigned ka[NS], ca[2 * NT];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) ka[s] = r32 * DP * 2 + 16 * ((2 * s + h) ^ swz<DP>(r32));
+  {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int colb = 32 * t + 16 * (g & 1) + 4 * (li & 3);
+      const int chunk = colb >> 3, half = (colb >> 2) & 1;
+      const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+      ca[2 * t] = r1 * DP * 2 + 16 * (chunk ^ swz<DP>(r1)) + 8 * half;
+      ca[2 * t + 1] = r2 * DP * 2 + 16 * (chunk ^ swz<DP>(r2)) + 8 * half;
+    }
+  }
+
+  f32x16 adq[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) adq[t] = zero16();
+  const int nkt = (a.Nk + 63) / 64;
+
+  kst.write(smem);
+  vst.write(smem + TILE);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; kt += 2) {
+#pragma unroll
+    for (int bsel = 0; bsel < 2; ++bsel) {
+      const int t = kt + bsel;
+      if (t >= nkt) break;
+      const char* ldsK = smem + bsel * 2 * TILE;
+      const char* ldsV = ldsK + TILE;
+      char* nxt = smem + (bsel ^ 1) * 2 * TILE;
+      const bool more = t + 1 < nkt;
+      if (more) {
+        kst.load(rk, (unsigned)(t + 1) * kstep);
+        vst.load(rv, (unsigned)(t + 1) * vstep);
+      }
+      const int nvalid = min(64, a.Nk - 64 * t);
+      if (active) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u == 1 && nvalid <= 32) break;
+          f32x16 sp = zero16(), dp = zero16();
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 kr = *reinterpret_cast<const bf16x8*>(ldsK + ka[s] + 32 * u * DP * 2);
+            const bf16x8 vr = *reinterpret_cast<const bf16x8*>(ldsV + ka[s] + 32 * u * DP * 2);
+            sp = MF<__bf16>::mma(kr, qf[s], sp);
+            dp = MF<__bf16>::mma(vr, gf[s], dp);
+          }
+          if (nvalid < 64) {   // tail: keys past the end contribute nothing
+            const int nvh = nvalid - 32 * u - 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sp[r] = ((r & 3) + 8 * (r >> 2)) < nvh ? sp[r] : -kInf;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = ex2(__builtin_fmaf(sp[r], sl2, lsc2));
+            dp[r] = p * (dp[r] - dlt);
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 sf = acc_frag<__bf16>(dp, s2);
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+              const int ro = (32 * u + 16 * s2) * DP * 2;
+              s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt] + ro));
+              s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt + 1] + ro));
+              typedef __attribute__((ext_vector_type(8))) short s16x8;
+              s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+              adq[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), sf, adq[tt]);
+            }
+          }
+        }
+      }
+      if (more) {
+        kst.write(nxt);
+        vst.write(nxt + TILE);
+      }
+      __syncthreads();
+    }
+  }
+  if (active) {
+    const int q0 = qb * BQ + w * 32;
+    __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
+    wave_store_rows<DP>(adq, a.scale, smem + w * 32 * DP * 2, DQ, a.dqs[1], a.Nq - q0, a.D, lane);
+  }
+}
+
+// --------------------------------------------------------------------------- dK / dV pass
+// One wave = 32 keys (key on the MFMA lane) with K, V fragments in registers; NW waves share
+// each 64-query Q / dO tile and its row constants (lse * log2 e, delta).  Per 32-query half:
+// S = Q K^T, dP = dO V^T (row reads), P = 2^(S sl2 - lse2), dS = P o (dP - delta),
+// dV^T += dO^T P and dK^T += Q^T dS (transposed reads of the dO / Q images).
+template <int DP, int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs a) {
+  using FF = F2<DP>;
+  constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
+  constexpr int BK = 32 * NW;
+  constexpr int TB = 2 * TILE + 2 * 64 * 4;   // [Q img | dO img | lse2[64] | delta[64]]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nkb = (a.Nk + BK - 1) / BK;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = bid % nkb;
+  bid /= nkb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int key = kb * BK + w * 32 + r32;
+  const bool active = kb * BK + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nk;
+  const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
+
+  F2Stage<DP, NW> qst, gst;
+  qst.init(tid, a.qs[1], a.D);
+  gst.init(tid, a.dos[1], a.D);
+  const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
+  const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
+  const unsigned qstep = (unsigned)(64 * a.qs[1] * 2), gstep = (unsigned)(64 * a.dos[1] * 2);
+  qst.load(rq, 0);
+  gst.load(rg, 0);
+  float rc_l = 0.f, rc_d = 0.f;   // row constants of the staged tile (threads 0..63)
+  auto fetch_rc = [&](int qt) {
+    if (tid < 64) {
+      const int qq = qt * 64 + tid;
+      rc_l = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
+      rc_d = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+    }
+  };
+  fetch_rc(0);
+
+  bf16x8 kf[NS], vf[NS];
+  {
+    const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+    const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+    const unsigned ko = (unsigned)((long long)key * a.ks[1] * 2);
+    const unsigned vo = (unsigned)((long long)key * a.vs[1] * 2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      const bool ok = d0 < a.D;
+      kf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, ok ? ko + d0 * 2 : 0x80000000u, 0, 0));
+      vf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, ok ? vo + d0 * 2 : 0x80000000u, 0, 0));
+    }
+  }
+  const float sl2 = a.scale * kLog2e;
+
+  unsigned ra[NS], ca[2 * NT];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) ra[s] = r32 * DP * 2 + 16 * ((2 * s + h) ^ swz<DP>(r32));
+  {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int colb = 32 * t + 16 * (g & 1) + 4 * (li & 3);
+      const int chunk = colb >> 3, half = (colb >> 2) & 1;
+      const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+      ca[2 * t] = r1 * DP * 2 + 16 * (chunk ^ swz<DP>(r1)) + 8 * half;
+      ca[2 * t + 1] = r2 * DP * 2 + 16 * (chunk ^ swz<DP>(r2)) + 8 * half;
+    }
+  }
+
+  f32x16 adk[NT], adv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    adk[t] = zero16();
+    adv[t] = zero16();
+  }
+  const int nqt = (a.Nq + 63) / 64;
+  auto put = [&](char* buf) {
+    qst.write(buf);
+    gst.write(buf + TILE);
+    if (tid < 64) {
+      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = rc_l;
+      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d;
+    }
+  };
+  put(smem);
+  __syncthreads();
+  for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
+#pragma unroll
+    for (int bsel = 0; bsel < 2; ++bsel) {
+      const int qt = qt0 + bsel;
+      if (qt >= nqt) break;
+      const char* ldsQ = smem + bsel * TB;
+      const char* ldsG = ldsQ + TILE;
+      const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
+      const float* ldsD = ldsL + 64;
+      char* nxt = smem + (bsel ^ 1) * TB;
+      const bool more = qt + 1 < nqt;
+      if (more) {
+        qst.load(rq, (unsigned)(qt + 1) * qstep);
+        gst.load(rg, (unsigned)(qt + 1) * gstep);
+        fetch_rc(qt + 1);
+      }
+      if (active) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u == 1 && qt * 64 + 32 >= a.Nq) break;
+          f32x16 sp = zero16(), dp = zero16();
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
+            const bf16x8 gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+            sp = MF<__bf16>::mma(qr, kf[s], sp);
+            dp = MF<__bf16>::mma(gr, vf[s], dp);
+          }
+          // rows q = 32u + row_of(r, h): constants for r = 4g + j at 32u + 8g + 4h + j
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float p = ex2(__builtin_fmaf(sp[4 * g + j], sl2, -l4[j]));
+              sp[4 * g + j] = p;
+              dp[4 * g + j] = p * (dp[4 * g + j] - d4[j]);
+            }
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 pf = acc_frag<__bf16>(sp, s2);
+            const bf16x8 sf = acc_frag<__bf16>(dp, s2);
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+              const int ro = (32 * u + 16 * s2) * DP * 2;
+              typedef __attribute__((ext_vector_type(8))) short s16x8;
+              s16x4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt] + ro));
+              s16x4 g2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt + 1] + ro));
+              s16x8 gv = {g1[0], g1[1], g1[2], g1[3], g2[0], g2[1], g2[2], g2[3]};
+              adv[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, gv), pf, adv[tt]);
+              s16x4 q1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt] + ro));
+              s16x4 q2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt + 1] + ro));
+              s16x8 qv = {q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+              adk[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, qv), sf, adk[tt]);
+            }
+          }
+        }
+      }
+      if (more) put(nxt);
+      __syncthreads();
+    }
+  }
+  if (active) {
+    const int k0 = kb * BK + w * 32;
+    char* scr = smem + w * 32 * DP * 2;
+    __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)k0 * a.dks[1];
+    __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)k0 * a.dvs[1];
+    wave_store_rows<DP>(adk, a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane);
+    wave_store_rows<DP>(adv, 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
+  }
+  (void)key;
+}
+
+}  // namespace sae

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <initializer_list>
 #include <string>
@@ -12,6 +13,8 @@
 #include "attn_kernels.h"
 #include "th_kernels.h"
 #include "variants.h"
+#include "fwd2.h"
+#include "bwd2.h"
 
 using namespace sae;
 
@@ -149,6 +152,68 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
     return check_launch("attn_fwd");
   }
 };
+
+// lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
+template <int DP, int NW, int MINW, bool LSUM> int fwd2_run(hipStream_t st, const AttnArgs& a) {
+  const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
+  const long long grid = (long long)nqb * a.H * a.B;
+  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  const size_t lds = 4 * (size_t)F2<DP>::TILE;
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
+  return check_launch("attn_fwd2");
+}
+
+// SAE_FWD_VARIANT (development A/B knob): "v1" = attn_fwd_kernel; default = fwd2 4 waves, MFMA row sum
+int fwd2_variant() {
+  const char* e = getenv("SAE_FWD_VARIANT");
+  if (!e || !*e) return 0;
+  return atoi(e[0] == 'v' ? e + 1 : e);
+}
+
+template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
+  switch (var) {
+    case 2: return fwd2_run<DP, 8, 2, true>(st, a);
+    case 3: return fwd2_run<DP, 8, 2, false>(st, a);
+    case 4: return fwd2_run<DP, 4, 2, true>(st, a);
+    case 5: return fwd2_run<DP, 4, 3, true>(st, a);
+    case 6: return fwd2_run<DP, 4, 3, false>(st, a);
+    default: return fwd2_run<DP, 4, 2, true>(st, a);
+  }
+}
+
+// lean bf16 backward (bwd2.h): dQ pass (publishes delta) then dK/dV pass
+template <int DP, int NWQ, int MQ, int NWK, int MK> int bwd2_run(hipStream_t st, const AttnArgs& a) {
+  {
+    const long long grid = (long long)((a.Nq + 32 * NWQ - 1) / (32 * NWQ)) * a.H * a.B;
+    if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+    const size_t lds = 4 * (size_t)F2<DP>::TILE;
+    if (int rc = lds_attr((const void*)attn_bwd2_dq_kernel<DP, NWQ, MQ>, lds)) return rc;
+    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, NWQ, MQ>), dim3((unsigned)grid), dim3(64 * NWQ), lds, st, a);
+    if (int rc = check_launch("attn_bwd2_dq")) return rc;
+  }
+  const long long grid = (long long)((a.Nk + 32 * NWK - 1) / (32 * NWK)) * a.H * a.B;
+  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512);
+  if (int rc = lds_attr((const void*)attn_bwd2_dkdv_kernel<DP, NWK, MK>, lds)) return rc;
+  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, NWK, MK>), dim3((unsigned)grid), dim3(64 * NWK), lds, st, a);
+  return check_launch("attn_bwd2_dkdv");
+}
+
+int bwd2_variant() {
+  const char* e = getenv("SAE_BWD_VARIANT");
+  if (!e || !*e) return 0;
+  return atoi(e[0] == 'v' ? e + 1 : e);
+}
+
+template <int DP> int bwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
+  switch (var) {
+    case 3: return bwd2_run<DP, 4, 3, 4, 2>(st, a);
+    case 4: return bwd2_run<DP, 8, 2, 8, 2>(st, a);
+    case 5: return bwd2_run<DP, 4, 2, 8, 2>(st, a);
+    default: return bwd2_run<DP, 4, 2, 4, 2>(st, a);
+  }
+}
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
   static int run(hipStream_t st, const AttnArgs& a) {
@@ -338,6 +403,15 @@ int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void
   const bool vec = d->head_dim % epc == 0 && strides_vec(d->q_stride, epc) && strides_vec(d->k_stride, epc) &&
                    strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o);
+  const int var = fwd2_variant();
+  if (const char* e = getenv("SAE_DBG")) a.dbg = atoi(e);
+  if (const char* e = getenv("SAE_DBG_BUF")) a.dbgbuf = (unsigned long long*)strtoull(e, nullptr, 16);
+  if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
+    const int dp = pick_dp(d->head_dim);
+    if (dp == 32) return fwd2_dispatch<32>((hipStream_t)stream, a, var);
+    if (dp == 64) return fwd2_dispatch<64>((hipStream_t)stream, a, var);
+    if (dp == 128) return fwd2_dispatch<128>((hipStream_t)stream, a, var);
+  }
   return dispatch<FwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }
 
@@ -358,6 +432,8 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
     return fail(SAE_EINVAL, "SAE_FLAG_RELPOS needs bias_h, bias_w, dbias_h, dbias_w");
   AttnArgs a;
   fill_args(a, d);
+  if (const char* e = getenv("SAE_DBG")) a.dbg = atoi(e);
+  if (const char* e = getenv("SAE_DBG_BUF")) a.dbgbuf = (unsigned long long*)strtoull(e, nullptr, 16);
   a.q = q;
   a.k = k;
   a.v = v;
@@ -379,6 +455,13 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
                    strides_vec(d->dk_stride, epc) && strides_vec(d->dv_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o) && aligned16(dout) && aligned16(dq) &&
                    aligned16(dk) && aligned16(dv);
+  const int var = bwd2_variant();
+  if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
+    const int dp = pick_dp(d->head_dim);
+    // head_dim 128 (BoTNet) stays on the v1 kernels: bwd2 at DP = 128 runs out of registers
+    if (dp == 32) return bwd2_dispatch<32>((hipStream_t)stream, a, var);
+    if (dp == 64) return bwd2_dispatch<64>((hipStream_t)stream, a, var);
+  }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }
 

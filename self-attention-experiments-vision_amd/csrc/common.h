@@ -185,9 +185,17 @@ template <typename T, int DP, int ROWS, bool VEC> struct Stage {
 
 // Buffer descriptor over rows [0, nrows) of a token-major tensor (row stride rs elements),
 // built from wave-uniform values only.
+// The inputs are passed through readfirstlane so that the compiler can PROVE the descriptor
+// wave-uniform and keep it in SGPRs (otherwise it wraps every buffer op in a waterfall loop,
+// cdna_hip_programming.md T20).
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const T* base, int nrows, long long rs) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long long)nrows * rs * sizeof(T)), 0x00020000);
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+  const int nbytes = __builtin_amdgcn_readfirstlane((int)((long long)nrows * rs * sizeof(T)));
+  void* pu = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pu, (short)0, nbytes, 0x00020000);
 }
 
 // Operand fragment read straight from global memory: row `row` of a token-major tensor,
@@ -231,6 +239,53 @@ __device__ __forceinline__ void store4(T* rowp, int d0, int D, float a, float b,
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (d0 + e < D) rowp[d0 + e] = (T)x[e];
+  }
+}
+
+// ------------------------------------------------------------------------ epilogue stores
+// A wave's 32 output rows held as NT accumulator tiles acc[t] = X^T (accumulator row = head-dim
+// column 32t + row_of(r, h), accumulator column = the wave's output row lane & 31), scaled by sc,
+// are written as bf16 rows into a per-wave LDS scratch of 32 x DP (XOR-swizzled like the tile
+// images: conflict-free 8-byte writes and 16-byte reads) and stored as whole 16-byte row chunks:
+// one wave-instruction covers 64 x 16 B = complete rows (8 rows of 128 B at DP = 64) instead of
+// 16 B slivers of 32 rows, so no partial cache lines are written at the row stride
+// (MI355X_MICROARCH.md "attention epilogue store tail").  Rows >= nrows and columns >= D are not
+// stored.  Wave-local: the scratch must not be in use by other waves.
+template <int DP>
+__device__ __forceinline__ void wave_store_rows(const f32x16* acc, float sc, char* scratch, __bf16* dst,
+                                                long long rs, int nrows, int D, int lane) {
+  constexpr int NT = DP / 32, CPR = DP / 8, RPI = 64 / CPR;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const bf16x4 v = {(__bf16)(acc[t][4 * g] * sc), (__bf16)(acc[t][4 * g + 1] * sc),
+                        (__bf16)(acc[t][4 * g + 2] * sc), (__bf16)(acc[t][4 * g + 3] * sc)};
+      *reinterpret_cast<bf16x4*>(scratch + r * DP * 2 + 16 * ((4 * t + g) ^ swz<DP>(r)) + 8 * h) = v;
+    }
+  __builtin_amdgcn_wave_barrier();
+  const int c = lane % CPR;
+#pragma unroll
+  for (int it = 0; it < 32 / RPI; ++it) {
+    const int rr = it * RPI + lane / CPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(scratch + rr * DP * 2 + 16 * (c ^ swz<DP>(rr)));
+    if (rr < nrows && c * 8 < D) *reinterpret_cast<uint4*>(dst + (long long)rr * rs + c * 8) = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------ diagnostic timestamps
+// Per-workgroup timeline (SAE_DBG & 64 only; never in a production launch): slot k of the
+// workgroup's 8-word record gets s_memrealtime (100 MHz); words 6/7 hold HW_ID and XCC_ID.
+__device__ __forceinline__ void wg_stamp(unsigned long long* buf, int dbg, int slot) {
+  if (!(dbg & 64) || threadIdx.x != 0) return;
+  unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  buf[blockIdx.x * 8 + slot] = t;
+  if (slot == 0) {
+    buf[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    buf[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 }
 

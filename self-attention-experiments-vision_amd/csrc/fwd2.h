@@ -1,0 +1,289 @@
+// fwd2.h -- lean bf16 forward attention for gfx950 (the hot path of every ViT/DeiT/CaiT layer).
+//
+// Same algorithm and layout as attn_fwd_kernel (attn_kernels.h; reference chain
+// models/layers/attentions/attention.py:39-58), re-built around the VALU budget of one
+// 32x32 score tile, which is what bounds a D <= 64 attention forward on CDNA4:
+//   * every per-tile address is precomputed once per thread: global offsets are 32-bit buffer
+//     offsets (hardware range check = zero fill for tail rows / padded head-dim columns), LDS
+//     read/write addresses are VGPR + immediate, the K/V tile loop is unrolled over the two
+//     LDS buffers so buffer selection is an immediate as well;
+//   * the softmax row sum l runs on the matrix pipe: an all-ones A operand turns the P^T fed
+//     to O^T = V^T P^T into one more MFMA per 16 keys whose accumulator rows are sum_k P
+//     (the 32 f32 adds per tile it replaces are the single largest VALU item after exp);
+//   * the running max uses v_max3 and one v_permlane32_swap for the lane-half exchange;
+//   * lazy rescale (T13, threshold 2^8) decided wave-uniformly before any P of the tile is
+//     exponentiated, as in the v1 kernel.
+// One wave owns 32 query rows (query on the MFMA lane, "swapped" S^T = K Q^T), NW waves share
+// each 64-key K/V tile staged global -> registers -> LDS (issue early, write late; one
+// barrier per tile).
+#pragma once
+#include "common.h"
+
+namespace sae {
+
+template <int DP> struct F2 {
+  static constexpr int NS = DP / 16;        // bf16 k-steps over the head dim
+  static constexpr int NT = DP / 32;        // 32-row tiles of O^T
+  static constexpr int CPR = DP / 8;        // 16-byte chunks per row
+  static constexpr int TILE = 64 * DP * 2;  // bytes of one 64-key image
+};
+
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int DP, int NW>
+struct F2Stage {
+  static constexpr int NCH = (64 * F2<DP>::CPR + 64 * NW - 1) / (64 * NW);
+  unsigned goff[NCH];   // byte offset inside a tile (0x80000000 = padded column: reads zero)
+  unsigned loff[NCH];   // LDS byte offset inside an image (0xffffffff = no chunk)
+  uint4 v[NCH];
+
+  __device__ __forceinline__ void init(int tid, long long rs, int D) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 64 * NW * i;
+      const int r = id / F2<DP>::CPR, c = id % F2<DP>::CPR;
+      const bool ok = id < 64 * F2<DP>::CPR;
+      goff[i] = (ok && c * 8 < D) ? (unsigned)(((long long)r * rs + c * 8) * 2) : 0x80000000u;
+      loff[i] = ok ? (unsigned)(r * DP * 2 + 16 * (c ^ swz<DP>(r))) : 0xffffffffu;
+    }
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned tileoff) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i] + tileoff, 0, 0));
+  }
+  __device__ __forceinline__ void write(char* img) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (64 * F2<DP>::CPR % (64 * NW) == 0 || loff[i] != 0xffffffffu)
+        *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
+  }
+};
+
+template <int DP, int NW, bool LSUM>
+__device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
+                                          f32x16& lacc, float& m, float& l, int nvalid, float sl2,
+                                          const unsigned* ka, const unsigned* va, int h) {
+  constexpr int NS = F2<DP>::NS, NT = F2<DP>::NT;
+  // nvalid: keys of this tile that exist (64 for every tile but the tail)
+  const bool two = nvalid > 32;
+  f32x16 s0 = zero16(), s1 = zero16();
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ldsK + ka[s]);
+    s0 = MF<__bf16>::mma(k0, qf[s], s0);
+  }
+  if (two) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ldsK + ka[s] + 32 * DP * 2);
+      s1 = MF<__bf16>::mma(k1, qf[s], s1);
+    }
+  }
+  if (nvalid < 64) {   // tail tile: keys past the end score -inf (key = row_of(r, h) = c_r + 4h)
+    const int nvh = nvalid - 4 * h;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = (r & 3) + 8 * (r >> 2);
+      s0[r] = c < nvh ? s0[r] : -kInf;
+      s1[r] = c + 32 < nvh ? s1[r] : -kInf;
+    }
+  }
+  float mx = s0[0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s0[r]);
+  if (two) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
+  }
+  mx = xhalf_max(mx) * sl2;
+  if (!__all(mx - m <= 8.f)) {
+    const float mn = fmaxf(m, mx);
+    const float alpha = ex2(m - mn);
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acco[t][r] *= alpha;
+    if constexpr (LSUM) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
+    } else {
+      l *= alpha;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s0[r] = ex2(__builtin_fmaf(s0[r], sl2, -m));
+  if (two) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s1[r] = ex2(__builtin_fmaf(s1[r], sl2, -m));
+  }
+  if constexpr (!LSUM) {
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ls += s0[r];
+    if (two) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ls += s1[r];
+    }
+    l += ls;
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 pf = acc_frag<__bf16>(s0, s2);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const char* p1 = ldsV + va[2 * t] + 16 * s2 * DP * 2;
+      const char* p2 = ldsV + va[2 * t + 1] + 16 * s2 * DP * 2;
+      s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+      s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+      acco[t] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), pf, acco[t]);
+    }
+    if constexpr (LSUM) lacc = MF<__bf16>::mma(ones, pf, lacc);
+  }
+  if (two) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = acc_frag<__bf16>(s1, s2);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const char* p1 = ldsV + va[2 * t] + (32 + 16 * s2) * DP * 2;
+        const char* p2 = ldsV + va[2 * t + 1] + (32 + 16 * s2) * DP * 2;
+        s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+        s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+        acco[t] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), pf, acco[t]);
+      }
+      if constexpr (LSUM) lacc = MF<__bf16>::mma(ones, pf, lacc);
+    }
+  }
+}
+
+template <int DP, int NW, int MINW, bool LSUM>
+__global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
+  using FF = F2<DP>;
+  constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
+  constexpr int BQ = 32 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (a.Nq + BQ - 1) / BQ;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb;
+  bid /= nqb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int q = qb * BQ + w * 32 + r32;
+  const bool active = qb * BQ + __builtin_amdgcn_readfirstlane(w) * 32 < a.Nq;
+
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+
+  wg_stamp(a.dbgbuf, a.dbg, 0);
+  if (a.dbg & 4) return;
+  F2Stage<DP, NW> kst, vst;
+  kst.init(tid, a.ks[1], a.D);
+  vst.init(tid, a.vs[1], a.D);
+  const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+  const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+  const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
+  kst.load(rk, 0);
+  vst.load(rv, 0);
+
+  // query fragments (row q, head-dim 16s + 8h .. +7), zero past Nq / D
+  bf16x8 qf[NS];
+  {
+    const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
+    const unsigned qo = (unsigned)((long long)q * a.qs[1] * 2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const unsigned off = (16 * s + 8 * h < a.D) ? qo + (16 * s + 8 * h) * 2 : 0x80000000u;
+      qf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0));
+    }
+  }
+  // per-lane LDS read addresses: K rows r32 (+32 as an immediate), V^T transposed reads
+  unsigned ka[NS], va[2 * NT];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) ka[s] = r32 * DP * 2 + 16 * ((2 * s + h) ^ swz<DP>(r32));
+  {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int colb = 32 * t + 16 * (g & 1) + 4 * (li & 3);
+      const int chunk = colb >> 3, half = (colb >> 2) & 1;
+      const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+      va[2 * t] = r1 * DP * 2 + 16 * (chunk ^ swz<DP>(r1)) + 8 * half;
+      va[2 * t + 1] = r2 * DP * 2 + 16 * (chunk ^ swz<DP>(r2)) + 8 * half;
+    }
+  }
+
+  f32x16 acco[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acco[t] = zero16();
+  f32x16 lacc = zero16();
+  float m = -kInf, l = 0.f;
+  const float sl2 = a.scale * kLog2e;
+  const int nkt = (a.Nk + 63) / 64;
+
+  kst.write(smem);
+  vst.write(smem + TILE);
+  __syncthreads();
+  wg_stamp(a.dbgbuf, a.dbg, 1);
+  // two tiles per trip: buffer 0 then buffer 1 (immediate LDS offsets)
+  for (int kt = 0; kt < nkt; kt += 2) {
+#pragma unroll
+    for (int bsel = 0; bsel < 2; ++bsel) {
+      const int t = kt + bsel;
+      if (t >= nkt) break;
+      char* cur = smem + bsel * 2 * TILE;
+      char* nxt = smem + (bsel ^ 1) * 2 * TILE;
+      const bool more = t + 1 < nkt;
+      if (more && !(a.dbg & 1)) {
+        kst.load(rk, (unsigned)(t + 1) * kstep);
+        vst.load(rv, (unsigned)(t + 1) * vstep);
+      }
+      if (active && !(a.dbg & 2))
+        fwd2_tile<DP, NW, LSUM>(cur, cur + TILE, qf, acco, lacc, m, l, min(64, a.Nk - 64 * t), sl2, ka, va, h);
+      if (more) {
+        kst.write(nxt);
+        vst.write(nxt + TILE);
+      }
+      __syncthreads();
+    }
+  }
+
+  wg_stamp(a.dbgbuf, a.dbg, 2);
+  if (!active || (a.dbg & 8)) return;
+  float lt;
+  if constexpr (LSUM) lt = lacc[0];
+  else lt = xhalf_sum(l);
+  const float inv = 1.f / lt;
+  {  // O rows through a per-wave LDS scratch (the K/V images are free after the last barrier)
+    const int q0 = qb * BQ + w * 32;
+    __bf16* O = reinterpret_cast<__bf16*>(a.out) + b * a.os[0] + hh * a.os[2] + (long long)q0 * a.os[1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acco[t][r] *= inv;
+    wave_store_rows<DP>(acco, 1.f, smem + w * 32 * DP * 2, O, a.os[1], a.Nq - q0, a.D, lane);
+  }
+  if (q < a.Nq && h == 0 && a.lse) a.lse[((size_t)b * a.H + hh) * a.Nq + q] = (m + lg2(lt)) * kLn2;
+  wg_stamp(a.dbgbuf, a.dbg, 3);
+}
+
+}  // namespace sae

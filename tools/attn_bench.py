@@ -3,7 +3,8 @@
 
     python tools/attn_bench.py [--iters 50] [--shapes deit_s,vitb384,...] [--dtype bf16]
 
-Times each C-ABI call with HIP events on the launch stream (median over iterations) and
+Times each C-ABI call inside HIP graphs of 10 back-to-back launches (HIP events around the
+replay, median over iterations, per-launch time = replay time / 10) and
 prints TFLOP/s and GB/s with the algorithmic counts of SURVEY §8d.
 """
 import argparse
@@ -53,17 +54,33 @@ def main():
         o, lse = ops._fwd(q, k, v, sc)
         ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
         torch.cuda.synchronize()
+        # HIP graphs of `reps` back-to-back launches: no host launch gaps inside the timed region
+        reps = 10
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                ops._fwd(q, k, v, sc)
+                ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+        torch.cuda.current_stream().wait_stream(s)
+        gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gf):
+            for _ in range(reps):
+                ops._fwd(q, k, v, sc)
+        with torch.cuda.graph(gb):
+            for _ in range(reps):
+                ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
         tf, tb = [], []
         for _ in range(args.iters):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
-            o, lse = ops._fwd(q, k, v, sc)
+            gf.replay()
             e[1].record()
-            ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+            gb.replay()
             e[2].record()
             torch.cuda.synchronize()
-            tf.append(e[0].elapsed_time(e[1]))
-            tb.append(e[1].elapsed_time(e[2]))
+            tf.append(e[0].elapsed_time(e[1]) / reps)
+            tb.append(e[1].elapsed_time(e[2]) / reps)
         tf.sort()
         tb.sort()
         mf, mb = tf[len(tf) // 2] / 1e3, tb[len(tb) // 2] / 1e3
