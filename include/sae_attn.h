@@ -142,6 +142,33 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* desc, const void* q, cons
                     const void* dout, void* dq, void* dk, void* dv, float* dth1,
                     float* dth2, void* workspace);
 
+/* Weight / bias gradients of a projection on the path (the Dense / DenseGeneral kernels of
+   attention.py:29-37,60-63 and ff.py:8-34, whose JAX autodiff computes them):
+     dw[i][j] (+)= sum_m x[m][i] * dy[m][j]      dw fp32 [I][J] (row stride ldw)
+     db[j]    (+)= sum_m dy[m][j]                db fp32 [J] (may be NULL)
+   x bf16 [M][I] (row stride ldx), dy bf16 [M][J] (row stride ldy); I, J, ldx, ldy multiples
+   of 8, pointers 16-byte aligned.  accumulate != 0 adds into dw / db.  Split over m with a
+   fixed-order reduction of the splits: deterministic, no atomics. */
+size_t sae_gemm_dw_workspace_bytes(int32_t M, int32_t I, int32_t J);
+int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx,
+                const void* dy, int64_t ldy, float* dw, int64_t ldw, float* db,
+                int32_t accumulate, void* workspace);
+
+/* Residual add + LayerNorm of the encoder blocks around the path (models/vit.py:19-31,57;
+   Flax nn.LayerNorm: fp32 statistics, eps, output in the compute dtype):
+     xout = x + delta (fp32; when delta != NULL), y = LN(xout) * gamma + beta in bf16,
+     mean / rstd fp32 [M] saved for the backward.  x, xout fp32 [M][C]; delta, y bf16 [M][C];
+     C a multiple of 4, <= 1024. */
+int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const void* delta,
+                      float* xout, const float* gamma, const float* beta, void* y, float* mean,
+                      float* rstd, float eps);
+size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C);
+/* dx = dxin + dLN/dx(dy) (fp32; dxin may be NULL), ddelta = bf16(dx) (may be NULL),
+   dgamma / dbeta fp32 [C] overwritten (fixed-order reduction, deterministic). */
+int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const float* mean,
+                      const float* rstd, const float* gamma, const void* dy, const float* dxin,
+                      float* dx, void* ddelta, float* dgamma, float* dbeta, void* workspace);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);
 

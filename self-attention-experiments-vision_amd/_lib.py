@@ -52,6 +52,11 @@ _PROTOS = [
     ("sae_th_attn_fwd", _i32, [_vp, ctypes.POINTER(SaeAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("sae_th_attn_bwd_workspace_bytes", _sz, [ctypes.POINTER(SaeAttnDesc)]),
     ("sae_th_attn_bwd", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 13),
+    ("sae_gemm_dw_workspace_bytes", _sz, [_i32, _i32, _i32]),
+    ("sae_gemm_dw", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
+    ("sae_layernorm_fwd", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32]),
+    ("sae_layernorm_bwd_workspace_bytes", _sz, [_i32, _i32]),
+    ("sae_layernorm_bwd", _i32, [_vp, _i32, _i32] + [_vp] * 11),
     ("sae_last_error", ctypes.c_char_p, []),
     ("sae_abi_version", _i32, []),
     ("sae_build_info", ctypes.c_char_p, []),

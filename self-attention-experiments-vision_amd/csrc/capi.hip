@@ -8,6 +8,7 @@
 #include <stdarg.h>
 #include <initializer_list>
 #include <string>
+#include <algorithm>
 
 #include "../../include/sae_attn.h"
 #include "attn_kernels.h"
@@ -15,6 +16,8 @@
 #include "variants.h"
 #include "fwd2.h"
 #include "bwd2.h"
+#include "gemm_dw.h"
+#include "ln.h"
 
 using namespace sae;
 
@@ -615,6 +618,158 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const v
   return th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace)
              ? fail(SAE_EHIP, "th_bwd launch failed")
              : check_launch("th_bwd");
+}
+
+// ------------------------------------------------------------------ projection gradients
+static void dw_plan(int M, int I, int J, int* S, int* chunk) {
+  const int tiles = ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
+  int s = (512 + tiles - 1) / tiles;
+  s = std::max(1, std::min(s, (M + 255) / 256));
+  int c = (M + s - 1) / s;
+  c = (c + kDwK - 1) / kDwK * kDwK;
+  *chunk = c;
+  *S = (M + c - 1) / c;
+}
+
+size_t sae_gemm_dw_workspace_bytes(int32_t M, int32_t I, int32_t J) {
+  if (M < 1 || I < 1 || J < 1) return 0;
+  int S, chunk;
+  dw_plan(M, I, J, &S, &chunk);
+  return (((size_t)S * I * J * 4 + 255) & ~(size_t)255) + (((size_t)S * J * 4 + 255) & ~(size_t)255);
+}
+
+int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx, const void* dy,
+                int64_t ldy, float* dw, int64_t ldw, float* db, int32_t accumulate, void* workspace) {
+  if (M < 1 || I < 1 || J < 1) return fail(SAE_EINVAL, "gemm_dw: M/I/J must be >= 1 (got %d/%d/%d)", M, I, J);
+  if (I % 8 || J % 8) return fail(SAE_EUNSUPPORTED, "gemm_dw: I (%d) and J (%d) must be multiples of 8", I, J);
+  if (ldx < I || ldy < J || ldw < J || ldx % 8 || ldy % 8 || ldw % 4)
+    return fail(SAE_EINVAL, "gemm_dw: bad leading dimensions ldx %lld ldy %lld ldw %lld", (long long)ldx,
+                (long long)ldy, (long long)ldw);
+  if (!x || !dy || !dw || !workspace) return fail(SAE_EINVAL, "gemm_dw: x/dy/dw/workspace must be non-NULL");
+  if (!aligned16(x) || !aligned16(dy) || !aligned16(dw) || !aligned16(workspace))
+    return fail(SAE_EINVAL, "gemm_dw: x, dy, dw and workspace must be 16-byte aligned");
+  DwArgs a;
+  memset(&a, 0, sizeof a);
+  a.x = reinterpret_cast<const __bf16*>(x);
+  a.dy = reinterpret_cast<const __bf16*>(dy);
+  a.M = M;
+  a.I = I;
+  a.J = J;
+  dw_plan(M, I, J, &a.S, &a.chunk);
+  if ((long long)a.chunk * std::max(ldx, ldy) * 2 >= (1LL << 31))
+    return fail(SAE_EUNSUPPORTED, "gemm_dw: token chunk exceeds 32-bit buffer addressing");
+  a.part = reinterpret_cast<float*>(workspace);
+  a.bpart = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) +
+                                     (((size_t)a.S * I * J * 4 + 255) & ~(size_t)255));
+  a.dw = dw;
+  a.db = db;
+  a.ldx = ldx;
+  a.ldy = ldy;
+  a.ldw = ldw;
+  a.accumulate = accumulate;
+  hipStream_t st = (hipStream_t)stream;
+  const long long grid = (long long)a.S * ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
+  const size_t lds = 4 * kDwK * 256;
+  if (int rc = lds_attr((const void*)gemm_dw_kernel<true>, lds)) return rc;
+  if (int rc = lds_attr((const void*)gemm_dw_kernel<false>, lds)) return rc;
+  if (db)
+    hipLaunchKernelGGL(gemm_dw_kernel<true>, dim3((unsigned)grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(gemm_dw_kernel<false>, dim3((unsigned)grid), dim3(256), lds, st, a);
+  if (int rc = check_launch("gemm_dw")) return rc;
+  const long long n4 = (long long)I * J / 4;
+  const unsigned rb = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3(rb, db ? 2 : 1), dim3(256), 0, st, a);
+  return check_launch("gemm_dw_reduce");
+}
+
+// ------------------------------------------------------------ residual add + LayerNorm
+static int ln_fwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 2048)); }
+static int ln_bwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 1024)); }
+
+static int ln_check(int32_t M, int32_t C) {
+  if (M < 1 || C < 4) return fail(SAE_EINVAL, "layernorm: M (%d) and C (%d) must be >= 1 / >= 4", M, C);
+  if (C % 4 || C > 4 * 64 * kLnMaxV)
+    return fail(SAE_EUNSUPPORTED, "layernorm: C (%d) must be a multiple of 4 and <= %d", C, 4 * 64 * kLnMaxV);
+  return SAE_OK;
+}
+
+int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const void* delta, float* xout,
+                      const float* gamma, const float* beta, void* y, float* mean, float* rstd, float eps) {
+  if (int rc = ln_check(M, C)) return rc;
+  if (!x || !gamma || !beta || !y || !mean || !rstd) return fail(SAE_EINVAL, "layernorm_fwd: NULL argument");
+  if ((delta == nullptr) != (xout == nullptr))
+    return fail(SAE_EINVAL, "layernorm_fwd: delta and xout must both be given or both be NULL");
+  if (!aligned16(x) || !aligned16(xout) || !aligned16(gamma) || !aligned16(beta) || ((uintptr_t)delta & 7) ||
+      ((uintptr_t)y & 7))
+    return fail(SAE_EINVAL, "layernorm_fwd: x/xout/gamma/beta need 16-byte, delta/y 8-byte alignment");
+  LnArgs a;
+  memset(&a, 0, sizeof a);
+  a.x = x;
+  a.delta = reinterpret_cast<const __bf16*>(delta);
+  a.xout = xout;
+  a.gamma = gamma;
+  a.beta = beta;
+  a.y = reinterpret_cast<__bf16*>(y);
+  a.mean = mean;
+  a.rstd = rstd;
+  a.M = M;
+  a.C = C;
+  a.eps = eps;
+  const int nv = (C / 4 + 63) / 64;
+  const dim3 g(ln_fwd_blocks(M)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, g, b, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, g, b, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, g, b, 0, st, a); break;
+  }
+  return check_launch("layernorm_fwd");
+}
+
+size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
+  if (M < 1 || C < 1) return 0;
+  return (size_t)ln_bwd_blocks(M) * 2 * C * sizeof(float);
+}
+
+int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
+                      const float* gamma, const void* dy, const float* dxin, float* dx, void* ddelta, float* dgamma,
+                      float* dbeta, void* workspace) {
+  if (int rc = ln_check(M, C)) return rc;
+  if (!x || !mean || !rstd || !gamma || !dy || !dx || !dgamma || !dbeta || !workspace)
+    return fail(SAE_EINVAL, "layernorm_bwd: NULL argument");
+  if (!aligned16(x) || !aligned16(dxin) || !aligned16(dx) || !aligned16(gamma) || !aligned16(workspace) ||
+      ((uintptr_t)dy & 7) || ((uintptr_t)ddelta & 7))
+    return fail(SAE_EINVAL, "layernorm_bwd: x/dxin/dx/gamma/workspace need 16-byte, dy/ddelta 8-byte alignment");
+  LnArgs a;
+  memset(&a, 0, sizeof a);
+  a.x = x;
+  a.mean = const_cast<float*>(mean);
+  a.rstd = const_cast<float*>(rstd);
+  a.gamma = gamma;
+  a.dy = reinterpret_cast<const __bf16*>(dy);
+  a.dxin = dxin;
+  a.dx = dx;
+  a.ddelta = reinterpret_cast<__bf16*>(ddelta);
+  a.part = reinterpret_cast<float*>(workspace);
+  a.dgamma = dgamma;
+  a.dbeta = dbeta;
+  a.M = M;
+  a.C = C;
+  a.nblk = ln_bwd_blocks(M);
+  const int nv = (C / 4 + 63) / 64;
+  const dim3 g(a.nblk), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, g, b, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, g, b, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, g, b, 0, st, a); break;
+  }
+  if (int rc = check_launch("layernorm_bwd")) return rc;
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64), dim3(256), 0, st, a);
+  return check_launch("layernorm_bwd_reduce");
 }
 
 const char* sae_last_error(void) { return g_err.c_str(); }

@@ -1,0 +1,212 @@
+// gemm_dw.h -- weight / bias gradients of the projections on the hot path, split over tokens.
+//
+// For every Dense / DenseGeneral of the path (QKV projection `queries|keys|values`,
+// attention.py:29-37; output projection `DenseGeneral_0`, attention.py:60-63; the FF block's
+// `Dense_0/1`, ff.py:8-34) the backward needs
+//     dW[i][j] = sum_m X[m][i] dY[m][j]      (fp32, the parameter dtype)
+//     db[j]    = sum_m dY[m][j]
+// with m running over every token of the batch (M = B*N = 25,216 for DeiT-S) and a small
+// output (384 x 1152 for the QKV projection).  Library GEMMs run this shape at 60-220 TF/s
+// (tools/gemm_probe.py); here it is a split-K MFMA kernel:
+//   * a workgroup owns a 128 x 128 output tile and one contiguous chunk of tokens; 4 waves,
+//     each a 64 x 64 quarter (2 x 2 accumulators of v_mfma_f32_32x32x16_bf16);
+//   * X and dY chunks of 64 tokens are staged global -> registers -> LDS as [token][column]
+//     images (XOR-swizzled 256-byte rows), double-buffered, and both MFMA operands are read
+//     with ds_read_b64_tr_b16 (K = tokens on the transposed axis, same permuted K order on both);
+//   * db rides on the matrix pipe: an all-ones A operand times the dY fragment gives column sums;
+//   * each split writes an fp32 partial tile; a second kernel sums the splits in a fixed order
+//     (deterministic, no atomics) and writes / accumulates the fp32 gradient.
+#pragma once
+#include "common.h"
+
+namespace sae {
+
+struct DwArgs {
+  const __bf16* x;    // [M][I] (row stride ldx elements)
+  const __bf16* dy;   // [M][J] (row stride ldy)
+  float* part;        // [S][I][J] fp32 partial sums
+  float* bpart;       // [S][J] fp32 partial bias sums (or null)
+  float* dw;          // [I][J] fp32 output (row stride ldw)
+  float* db;          // [J] fp32 output (or null)
+  int M, I, J, S, chunk;   // chunk = tokens per split (multiple of 64)
+  long long ldx, ldy, ldw;
+  int accumulate;     // dw / db += instead of =
+};
+
+constexpr int kDwT = 128;   // output tile edge
+constexpr int kDwK = 64;    // tokens per staged stage
+
+// tile images: [64 tokens][128 columns] bf16, 256-byte rows, swz<128>
+template <int NCH>
+struct DwStage {
+  uint4 v[NCH];
+  unsigned goff[NCH];
+  unsigned loff[NCH];
+  __device__ __forceinline__ void init(int tid, long long ld, int col0, int ncols) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 256 * i;
+      const int r = id >> 4, c = id & 15;
+      goff[i] = (col0 + 8 * c < ncols) ? (unsigned)(((long long)r * ld + col0 + 8 * c) * 2) : 0x80000000u;
+      loff[i] = r * 256 + 16 * (c ^ swz<128>(r));
+    }
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned rowoff) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i] + rowoff, 0, 0));
+  }
+  __device__ __forceinline__ void write(char* img) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
+  }
+};
+
+// transposed operand read: column col0 + (lane & 31) on the lane, K over rows 16s + permuted
+__device__ __forceinline__ bf16x8 dw_colfrag(const char* img, const unsigned* ca, int s, int t) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const int ro = 16 * s * 256;
+  s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ca[2 * t] + ro));
+  s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ca[2 * t + 1] + ro));
+  s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool BIAS>
+__global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = kDwK * 256;     // 16 KiB per operand image
+  const int ti = (a.I + kDwT - 1) / kDwT;
+  int bid = blockIdx.x;
+  const int s = bid % a.S;            // consecutive blocks = splits of one tile
+  bid /= a.S;
+  const int it = bid % ti, jt = bid / ti;
+  const int i0 = it * kDwT, j0 = jt * kDwT;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = w & 1, wj = w >> 1;  // this wave's 64 x 64 quarter
+  const int m0 = s * a.chunk;
+  const int m1 = min(a.M, m0 + a.chunk);
+  const bool bias = BIAS && it == 0 && wi == 0;
+
+  // row ranges [m0, m1) of X and dY through buffer descriptors (rows past m1 read zero)
+  const __amdgpu_buffer_rsrc_t rx = row_rsrc(a.x + (long long)m0 * a.ldx, m1 - m0, a.ldx);
+  const __amdgpu_buffer_rsrc_t ry = row_rsrc(a.dy + (long long)m0 * a.ldy, m1 - m0, a.ldy);
+  DwStage<4> xs, ys;
+  xs.init(tid, a.ldx, i0, a.I);
+  ys.init(tid, a.ldy, j0, a.J);
+  const unsigned xstep = (unsigned)(kDwK * a.ldx * 2), ystep = (unsigned)(kDwK * a.ldy * 2);
+  xs.load(rx, 0);
+  ys.load(ry, 0);
+
+  unsigned ca[8];   // [operand x / dy][t = 0, 1][r1, r2] transposed-read addresses
+  {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const int col0 = 64 * (op == 0 ? wi : wj) + 32 * t;
+        const int colb = col0 + 16 * (g & 1) + 4 * (li & 3);
+        const int chunk = colb >> 3, half = (colb >> 2) & 1;
+        const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+        ca[4 * op + 2 * t] = r1 * 256 + 16 * (chunk ^ swz<128>(r1)) + 8 * half;
+        ca[4 * op + 2 * t + 1] = r2 * 256 + 16 * (chunk ^ swz<128>(r2)) + 8 * half;
+      }
+    }
+  }
+  f32x16 acc[2][2], accb[2];
+#pragma unroll
+  for (int a2 = 0; a2 < 2; ++a2) {
+    accb[a2] = zero16();
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) acc[a2][b2] = zero16();
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+
+  const int nst = (m1 - m0 + kDwK - 1) / kDwK;
+  xs.write(smem);
+  ys.write(smem + IMG);
+  __syncthreads();
+  for (int st0 = 0; st0 < nst; st0 += 2) {
+#pragma unroll
+    for (int bsel = 0; bsel < 2; ++bsel) {
+      const int st = st0 + bsel;
+      if (st >= nst) break;
+      const char* imx = smem + bsel * 2 * IMG;
+      const char* imy = imx + IMG;
+      char* nxt = smem + (bsel ^ 1) * 2 * IMG;
+      const bool more = st + 1 < nst;
+      if (more) {
+        xs.load(rx, (unsigned)(st + 1) * xstep);
+        ys.load(ry, (unsigned)(st + 1) * ystep);
+      }
+#pragma unroll
+      for (int k = 0; k < kDwK / 16; ++k) {
+        const bf16x8 a0 = dw_colfrag(imx, ca, k, 0), a1 = dw_colfrag(imx, ca, k, 1);
+        const bf16x8 b0 = dw_colfrag(imy, ca + 4, k, 0), b1 = dw_colfrag(imy, ca + 4, k, 1);
+        acc[0][0] = MF<__bf16>::mma(a0, b0, acc[0][0]);
+        acc[0][1] = MF<__bf16>::mma(a0, b1, acc[0][1]);
+        acc[1][0] = MF<__bf16>::mma(a1, b0, acc[1][0]);
+        acc[1][1] = MF<__bf16>::mma(a1, b1, acc[1][1]);
+        if (bias) {
+          accb[0] = MF<__bf16>::mma(ones, b0, accb[0]);
+          accb[1] = MF<__bf16>::mma(ones, b1, accb[1]);
+        }
+      }
+      if (more) {
+        xs.write(nxt);
+        ys.write(nxt + IMG);
+      }
+      __syncthreads();
+    }
+  }
+  // fp32 partial tile: accumulator row = i (row_of), column = j (lane)
+  float* P = a.part + (size_t)s * a.I * a.J;
+  const int jc = j0 + 64 * wj + (lane & 31);
+#pragma unroll
+  for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) {
+      const int j = jc + 32 * b2;
+      if (j >= a.J) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + 64 * wi + 32 * a2 + row_of(r, h);
+        if (i < a.I) P[(size_t)i * a.J + j] = acc[a2][b2][r];
+      }
+    }
+  if (bias && h == 0) {
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) {
+      const int j = jc + 32 * b2;
+      if (j < a.J) a.bpart[(size_t)s * a.J + j] = accb[b2][0];
+    }
+  }
+}
+
+// dw[i][j] (+)= sum_s part[s][i][j] in split order; db likewise (blockIdx.y == 1 for db)
+__global__ __launch_bounds__(256) void gemm_dw_reduce_kernel(DwArgs a) {
+  if (blockIdx.y == 0) {
+    const long long n4 = (long long)a.I * a.J / 4;
+    const long long stride = (long long)a.I * a.J;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n4; e += (long long)gridDim.x * 256) {
+      f32x4 acc = *reinterpret_cast<const f32x4*>(a.part + 4 * e);
+      for (int s = 1; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(a.part + s * stride + 4 * e);
+      const long long i = (4 * e) / a.J, j = (4 * e) % a.J;
+      f32x4* out = reinterpret_cast<f32x4*>(a.dw + i * a.ldw + j);
+      if (a.accumulate) acc += *out;
+      *out = acc;
+    }
+  } else if (a.db) {
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < a.J; j += gridDim.x * 256) {
+      float acc = a.bpart[j];
+      for (int s = 1; s < a.S; ++s) acc += a.bpart[(size_t)s * a.J + j];
+      a.db[j] = a.accumulate ? a.db[j] + acc : acc;
+    }
+  }
+}
+
+}  // namespace sae

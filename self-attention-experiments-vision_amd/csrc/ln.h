@@ -1,0 +1,200 @@
+// ln.h -- the EncoderBlock glue around the attention hot path: residual add + LayerNorm.
+//
+// Reference: models/vit.py:19-31 (x = LN(inputs); x = attn(x) + inputs; y = LN(x); FF(y) + x)
+// and vit.py:57 (final LayerNorm), Flax nn.LayerNorm(dtype): epsilon 1e-6, statistics in fp32,
+// y = (x - mean) * rsqrt(var + eps) * scale + bias, output in the compute dtype.  Every residual
+// add of the encoder is followed by a LayerNorm (the next block's LN0 or the final one), so one
+// kernel does both:
+//     x_out = x + delta            (fp32 residual stream; delta = attention / FF output, bf16)
+//     y     = LN(x_out) in bf16    (+ per-row mean, rstd kept for the backward)
+// and the backward
+//     dx    = dx_in + LN_bwd(dy)   (fp32; the gradient of x and, cast to bf16, of delta)
+//     dscale, dbias: per-workgroup partials, summed in a fixed order by a second kernel.
+// One wave per row (C <= 1024 columns, float4 per lane), rows strided over the grid; HBM-bound.
+#pragma once
+#include "common.h"
+
+namespace sae {
+
+struct LnArgs {
+  const float* x;        // [M][C] fp32 residual stream in
+  const __bf16* delta;   // [M][C] bf16 addend (or null)
+  float* xout;           // [M][C] fp32 x + delta (null if no delta)
+  const float* gamma;    // [C] LayerNorm scale
+  const float* beta;     // [C] LayerNorm bias
+  __bf16* y;             // [M][C] bf16 output
+  float* mean;           // [M]
+  float* rstd;           // [M]
+  // backward
+  const __bf16* dy;      // [M][C] gradient of y
+  const float* dxin;     // [M][C] gradient arriving at x_out from its other consumers (or null)
+  float* dx;             // [M][C] fp32 gradient of x (and of delta)
+  __bf16* ddelta;        // [M][C] bf16 copy of dx for delta (or null)
+  float* part;           // [nblk][2][C] per-workgroup dscale / dbias partials
+  float* dgamma;         // [C]
+  float* dbeta;          // [C]
+  int M, C, nblk;
+  float eps;
+};
+
+constexpr int kLnMaxV = 4;   // float4 chunks per lane: C <= 1024
+
+__device__ __forceinline__ float ln_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ f32x4 ld_bf16x4(const __bf16* p) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+__device__ __forceinline__ void st_bf16x4(__bf16* p, f32x4 v) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int C4 = a.C >> 2;
+  f32x4 g[NV], bt[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = lane + 64 * k;
+    g[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.gamma)[c] : f32x4{};
+    bt[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.beta)[c] : f32x4{};
+  }
+  const float invC = 1.f / (float)a.C;
+  for (int row = wave; row < a.M; row += nw) {
+    const size_t ro = (size_t)row * a.C;
+    f32x4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = lane + 64 * k;
+      v[k] = f32x4{};
+      if (c < C4) {
+        v[k] = reinterpret_cast<const f32x4*>(a.x + ro)[c];
+        if (a.delta) {
+          v[k] += ld_bf16x4(a.delta + ro + 4 * c);
+          reinterpret_cast<f32x4*>(a.xout + ro)[c] = v[k];
+        }
+      }
+      s += v[k][0] + v[k][1] + v[k][2] + v[k][3];
+    }
+    const float mu = ln_wave_sum(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = lane + 64 * k;
+      if (c < C4) {
+        const f32x4 d = v[k] - mu;
+        q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+      }
+    }
+    const float rs = __builtin_amdgcn_rsqf(ln_wave_sum(q) * invC + a.eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = lane + 64 * k;
+      if (c < C4) st_bf16x4(a.y + ro + 4 * c, (v[k] - mu) * rs * g[k] + bt[k]);
+    }
+    if (lane == 0) {
+      a.mean[row] = mu;
+      a.rstd[row] = rs;
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
+  __shared__ f32x4 red[4][2][64 * NV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wave = blockIdx.x * 4 + w;
+  const int nw = gridDim.x * 4;
+  const int C4 = a.C >> 2;
+  f32x4 g[NV], pg[NV], pb[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = lane + 64 * k;
+    g[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.gamma)[c] : f32x4{};
+    pg[k] = pb[k] = f32x4{};
+  }
+  const float invC = 1.f / (float)a.C;
+  for (int row = wave; row < a.M; row += nw) {
+    const size_t ro = (size_t)row * a.C;
+    const float mu = a.mean[row], rs = a.rstd[row];
+    f32x4 xh[NV], gy[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = lane + 64 * k;
+      xh[k] = gy[k] = f32x4{};
+      if (c < C4) {
+        const f32x4 dyv = ld_bf16x4(a.dy + ro + 4 * c);
+        xh[k] = (reinterpret_cast<const f32x4*>(a.x + ro)[c] - mu) * rs;
+        gy[k] = dyv * g[k];
+        pg[k] += dyv * xh[k];
+        pb[k] += dyv;
+      }
+      s1 += gy[k][0] + gy[k][1] + gy[k][2] + gy[k][3];
+      const f32x4 t = gy[k] * xh[k];
+      s2 += t[0] + t[1] + t[2] + t[3];
+    }
+    const float m1 = ln_wave_sum(s1) * invC, m2 = ln_wave_sum(s2) * invC;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = lane + 64 * k;
+      if (c < C4) {
+        f32x4 d = (gy[k] - m1 - xh[k] * m2) * rs;
+        if (a.dxin) d += reinterpret_cast<const f32x4*>(a.dxin + ro)[c];
+        reinterpret_cast<f32x4*>(a.dx + ro)[c] = d;
+        if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d);
+      }
+    }
+  }
+  // workgroup partial: the 4 waves' sums added in wave order
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    red[w][0][lane + 64 * k] = pg[k];
+    red[w][1][lane + 64 * k] = pb[k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C4; i += 256) {
+    const int which = i / C4, c = i % C4;
+    f32x4 s = red[0][which][c];
+    s += red[1][which][c];
+    s += red[2][which][c];
+    s += red[3][which][c];
+    reinterpret_cast<f32x4*>(a.part + ((size_t)blockIdx.x * 2 + which) * a.C)[c] = s;
+  }
+}
+
+// dgamma / dbeta = sum of the workgroup partials in workgroup order (deterministic):
+// 256 threads = 64 columns x 4 strided groups, then the 4 group sums in order.
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a) {
+  __shared__ float red[4][2][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float sg = 0.f, sb = 0.f;
+  if (c < a.C) {
+#pragma unroll 8
+    for (int b = grp; b < a.nblk; b += 4) {
+      sg += a.part[((size_t)b * 2) * a.C + c];
+      sb += a.part[((size_t)b * 2 + 1) * a.C + c];
+    }
+  }
+  red[grp][0][cl] = sg;
+  red[grp][1][cl] = sb;
+  __syncthreads();
+  if (grp == 0 && c < a.C) {
+    a.dgamma[c] = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+    a.dbeta[c] = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+  }
+}
+
+}  // namespace sae

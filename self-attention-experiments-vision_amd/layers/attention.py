@@ -11,10 +11,11 @@ Same dataclass fields, same call signatures (``(inputs_q, inputs_kv, is_training
 cast to ``dtype`` for compute like Flax's DenseGeneral.  Parameters are created at
 construction when ``in_ch`` is given, otherwise at the first call (Flax ``init`` semantics).
 
-Compute path: projections are plain GEMMs (hipBLASLt through torch.matmul; the self-attention
-Q/K/V projection is ONE GEMM producing a packed [B, N, 3, H, D] buffer that the attention
-kernel reads in place by strides); the attention core is the fused HIP kernel
-(``ops.attention*``).  There is no eager/CPU fallback.
+Compute path: projections go through ``ops.dense`` (forward and input gradient on the library
+GEMM, weight / bias gradients straight into fp32 by the split-token MFMA kernel
+``sae_gemm_dw``); the self-attention Q/K/V projection is ONE GEMM producing a packed
+[B, N, 3, H, D] buffer that the attention kernel reads in place by strides; the attention core
+is the fused HIP kernel (``ops.attention*``).  There is no eager/CPU fallback.
 """
 from __future__ import annotations
 
@@ -125,35 +126,34 @@ class AttentionBlock(nn.Module):
         Nk = inputs_kv.shape[1]
         xq = inputs_q.to(dt)
         scale = 1.0 / math.sqrt(D)
-        wq, wk, wv = (m.kernel.to(dt) for m in (self.queries, self.keys, self.values))
+        HD = H * D
+        wq, wk, wv = (m.kernel for m in (self.queries, self.keys, self.values))     # fp32 [C, H, D]
+        bias = (lambda *ms: torch.stack([m.bias for m in ms], 0).reshape(-1)) if self.use_bias else None
         self_attn = inputs_q is inputs_kv
         if self_attn:
-            w = torch.stack((wq, wk, wv), dim=1).reshape(C, 3 * H * D)
-            qkv = (xq @ w).view(B, Nq, 3, H, D)
-            if self.use_bias:
-                qkv = qkv + torch.stack([m.bias.to(dt) for m in (self.queries, self.keys, self.values)], 0)
+            # ONE projection GEMM producing the packed [B, N, 3, H, D] buffer the kernels read in place
+            w = torch.stack((wq, wk, wv), dim=1).reshape(C, 3 * HD)
+            qkv = ops.dense(xq, w, bias(self.queries, self.keys, self.values) if bias else None, dt)
+            qkv = qkv.view(B, Nq, 3, H, D)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         else:
             xkv = inputs_kv.to(dt)
-            q = (xq @ wq.reshape(C, H * D)).view(B, Nq, H, D)
-            kv = (xkv @ torch.stack((wk, wv), dim=1).reshape(C, 2 * H * D)).view(B, Nk, 2, H, D)
-            if self.use_bias:
-                q = q + self.queries.bias.to(dt)
-                kv = kv + torch.stack([self.keys.bias.to(dt), self.values.bias.to(dt)], 0)
+            q = ops.dense(xq, wq.reshape(C, HD), self.queries.bias.reshape(-1) if bias else None, dt)
+            q = q.view(B, Nq, H, D)
+            kv = ops.dense(xkv, torch.stack((wk, wv), dim=1).reshape(C, 2 * HD),
+                           bias(self.keys, self.values) if bias else None, dt).view(B, Nk, 2, H, D)
             k, v = kv[:, :, 0], kv[:, :, 1]
         if self.rotary:
             q, k = ops.rotary(q), ops.rotary(k)
         if self.talking_heads:
             o = ops.talking_heads_attention(q, k, v, self.TalkingHeadsBlock_0.talking_heads_transform,
                                             self.TalkingHeadsBlock_1.talking_heads_transform, scale)
-        elif self_attn and not self.rotary and not self.use_bias:
+        elif self_attn and not self.rotary:
             o = ops.attention_packed(qkv, scale)
         else:
             o = ops.attention(q, k, v, scale)
-        wo = self.DenseGeneral_0.kernel.to(dt).reshape(H * D, self._out_ch_eff)
-        y = o.reshape(B, Nq, H * D) @ wo
-        if self.use_bias:
-            y = y + self.DenseGeneral_0.bias.to(dt)
+        wo = self.DenseGeneral_0.kernel.reshape(HD, self._out_ch_eff)
+        y = ops.dense(o.reshape(B, Nq, HD), wo, self.DenseGeneral_0.bias if self.use_bias else None, dt)
         if self.out_dropout_rate > 0.0:
             y = F.dropout(y, p=self.out_dropout_rate, training=is_training)
         return y

@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "talking_heads_attention", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -353,3 +353,152 @@ def rotary(x: torch.Tensor, base: float = 10000.0) -> torch.Tensor:
     """GPT-J interleaved rotary on [B, N, H, D] (position_embed.py:8-20; build-defined base
     10000, survey D6)."""
     return _Rotary.apply(x, float(base))
+
+
+# ------------------------------------------------------------------------------ projections
+def gemm_dw(x2: torch.Tensor, dy2: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor] = None,
+            accumulate: bool = False) -> None:
+    """dw (+)= x2^T dy2 and db (+)= colsum(dy2) in fp32 through ``sae_gemm_dw`` (split over the
+    token axis, fixed-order reduction).  x2 [M, I], dy2 [M, J] bf16 with unit column stride."""
+    lib = L.load()
+    _require_gpu(x2, dy2, dw)
+    M, I = x2.shape
+    J = dy2.shape[1]
+    ws = torch.empty(lib.sae_gemm_dw_workspace_bytes(M, I, J), dtype=torch.uint8, device=x2.device)
+    tok = _TIMER.begin("gemm_dw") if _TIMER is not None else None
+    L.check(lib.sae_gemm_dw(_stream(x2), M, I, J, _ptr(x2), x2.stride(0), _ptr(dy2), dy2.stride(0), _ptr(dw),
+                            dw.stride(0), _ptr(db), int(accumulate), _ptr(ws)))
+    if tok is not None:
+        _TIMER.end(tok, (M, I, J))
+
+
+def _dw_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
+    return (x2.is_cuda and x2.dtype == dy2.dtype == torch.bfloat16 and x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0
+            and x2.stride(1) == 1 and dy2.stride(1) == 1 and x2.stride(0) % 8 == 0 and dy2.stride(0) % 8 == 0
+            and x2.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0)
+
+
+class _Dense(torch.autograd.Function):
+    """y = x @ W (+ b): Flax ``Dense`` / ``DenseGeneral`` semantics (input and fp32 kernel cast to
+    the compute dtype).  Backward: dX = dY W^T (library GEMM), dW / db straight into fp32 by the
+    split-token MFMA kernel (``sae_gemm_dw``) when the compute dtype is bf16."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dt):
+        I, J = w.shape
+        wd = w.to(dt)
+        x2 = x.to(dt).reshape(-1, I)
+        y = x2 @ wd
+        if b is not None:
+            y = y + b.to(dt)
+        ctx.save_for_backward(x2, wd)
+        ctx.has_b, ctx.xshape, ctx.wdtype, ctx.xdtype = b is not None, x.shape, w.dtype, x.dtype
+        return y.view(*x.shape[:-1], J)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wd = ctx.saved_tensors
+        I, J = wd.shape
+        dy2 = dy.reshape(-1, J)
+        if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+            dy2 = dy2.contiguous()
+        dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
+        if _dw_ok(x2, dy2):
+            dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
+            db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
+            gemm_dw(x2, dy2, dw, db)
+            dw = dw.to(ctx.wdtype)
+        else:
+            dw = (x2.t() @ dy2).to(ctx.wdtype)
+            db = dy2.sum(0, dtype=torch.float32) if ctx.has_b else None
+        return dx, dw, db, None
+
+
+def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
+    """Projection of the hot path: ``x @ w (+ b)`` in ``dtype`` with fp32 parameter gradients."""
+    return _Dense.apply(x, w, b, dtype)
+
+
+# ------------------------------------------------------------------ residual add + LayerNorm
+LN_EPS = 1e-6   # Flax nn.LayerNorm default (models/vit.py:19,26,57)
+
+
+def layer_norm_ok(x: torch.Tensor) -> bool:
+    """The fused kernels cover the encoder's fp32 residual stream with C % 4 == 0, C <= 1024."""
+    C = x.shape[-1]
+    return x.is_cuda and x.dtype == torch.float32 and C % 4 == 0 and C <= 1024 and x.is_contiguous()
+
+
+def _ln_fwd(x, delta, gamma, beta, eps):
+    lib = L.load()
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    xout = torch.empty_like(x) if delta is not None else None
+    L.check(lib.sae_layernorm_fwd(_stream(x), M, C, _ptr(x), _ptr(delta), _ptr(xout), _ptr(gamma), _ptr(beta),
+                                  _ptr(y), _ptr(mean), _ptr(rstd), float(eps)))
+    return xout, y, mean, rstd
+
+
+def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta):
+    lib = L.load()
+    C = xs.shape[-1]
+    M = xs.numel() // C
+    dy = dy.contiguous()
+    dx = torch.empty_like(xs)
+    ddelta = torch.empty(xs.shape, dtype=torch.bfloat16, device=xs.device) if want_ddelta else None
+    dg = torch.empty(C, dtype=torch.float32, device=xs.device)
+    db = torch.empty(C, dtype=torch.float32, device=xs.device)
+    ws = torch.empty(lib.sae_layernorm_bwd_workspace_bytes(M, C), dtype=torch.uint8, device=xs.device)
+    if dxin is not None:
+        dxin = dxin.contiguous()
+    L.check(lib.sae_layernorm_bwd(_stream(xs), M, C, _ptr(xs), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dy),
+                                  _ptr(dxin), _ptr(dx), _ptr(ddelta), _ptr(dg), _ptr(db), _ptr(ws)))
+    return dx, ddelta, dg, db
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        _, y, mean, rstd = _ln_fwd(x, None, gamma, beta, eps)
+        ctx.save_for_backward(x, mean, rstd, gamma)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, gamma = ctx.saved_tensors
+        dx, _, dg, db = _ln_bwd(x, mean, rstd, gamma, dy, None, False)
+        return dx, dg, db, None
+
+
+class _AddLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, delta, gamma, beta, eps):
+        xout, y, mean, rstd = _ln_fwd(x, delta.contiguous(), gamma, beta, eps)
+        ctx.save_for_backward(xout, mean, rstd, gamma)
+        ctx.delta_dtype = delta.dtype
+        return xout, y
+
+    @staticmethod
+    def backward(ctx, dxout, dy):
+        xout, mean, rstd, gamma = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros(xout.shape, dtype=torch.bfloat16, device=xout.device)
+        dx, ddelta, dg, db = _ln_bwd(xout, mean, rstd, gamma, dy, dxout, True)
+        return dx, ddelta.to(ctx.delta_dtype), dg, db, None
+
+
+def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = LN_EPS) -> torch.Tensor:
+    """Flax ``nn.LayerNorm(dtype=bfloat16)`` of an fp32 residual stream: bf16 output (HIP kernel)."""
+    _require_gpu(x)
+    return _LayerNorm.apply(x, gamma, beta, eps)
+
+
+def add_layer_norm(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                   eps: float = LN_EPS):
+    """``x + delta`` (fp32 residual add, models/vit.py:24,31) and its LayerNorm in bf16, one kernel;
+    returns ``(x + delta, LN(x + delta))``."""
+    _require_gpu(x, delta)
+    return _AddLayerNorm.apply(x, delta, gamma, beta, eps)

@@ -9,8 +9,10 @@ reference's mixed precision: fp32 params, ``dtype`` compute, fp32 residual strea
 cls / pos-embed params promote it, vit.py:46,85), LayerNorm eps 1e-6, tanh-GELU (Flax
 ``nn.gelu`` default).
 
-The attention is ``layers.SelfAttentionBlock`` (fused HIP kernels); LayerNorm, GELU and the
-Dense GEMMs are library ops (survey §8f ranks them "next").
+The attention is ``layers.SelfAttentionBlock`` (fused HIP kernels).  Around it (survey §8f
+"next"): Dense / DenseGeneral go through ``ops.dense`` (library GEMM forward and input gradient,
+HIP split-token weight/bias gradients), and with a bf16 compute dtype every residual add is fused
+with the LayerNorm that follows it (``ops.add_layer_norm``, HIP); GELU stays a library op.
 """
 from __future__ import annotations
 
@@ -21,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
 from .layers.attention import DenseGeneral, SelfAttentionBlock, lecun_normal_
 
 __all__ = ["ViT", "create_model", "MODEL_CONFIGS", "vit_flops_per_image"]
@@ -38,8 +41,7 @@ class Dense(nn.Module):
         self.bias = nn.Parameter(torch.zeros(features, device=device)) if use_bias else None
 
     def forward(self, x, dtype):
-        y = x.to(dtype) @ self.kernel.to(dtype)
-        return y + self.bias.to(dtype) if self.bias is not None else y
+        return ops.dense(x, self.kernel, self.bias, dtype)
 
 
 class LayerNorm(nn.Module):
@@ -100,8 +102,20 @@ class Encoder(nn.Module):
 
     def forward(self, inputs, is_training):
         x = inputs.float() + self.AddAbsPosEmbed_0.pos_embed
-        for i in range(self.num_layers):
-            x = getattr(self, f"EncoderBlock_{i}")(x, is_training)
+        blocks = [getattr(self, f"EncoderBlock_{i}") for i in range(self.num_layers)]
+        if self.dtype == torch.bfloat16 and blocks and ops.layer_norm_ok(x):
+            # Same math as vit.py:19-31,57, with every residual add fused into the LayerNorm that
+            # follows it (the next block's LayerNorm_0, or the final one): one HBM pass each.
+            h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
+            for i, blk in enumerate(blocks):
+                a = blk.SelfAttentionBlock_0(h, is_training=is_training)
+                x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
+                f = blk.FFBlock_0(h, self.dtype)
+                nxt = blocks[i + 1].LayerNorm_0 if i + 1 < len(blocks) else self.LayerNorm_0
+                x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+            return h
+        for blk in blocks:
+            x = blk(x, is_training)
         return self.LayerNorm_0(x, self.dtype)
 
 

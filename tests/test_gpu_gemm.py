@@ -1,0 +1,83 @@
+"""Projection-gradient kernel (sae_gemm_dw) against a float64 reference of the same bf16 inputs.
+
+dW = X^T dY and db = colsum(dY) are what the JAX autodiff of the reference's Dense /
+DenseGeneral projections computes (attention.py:29-37,60-63; ff.py:8-34); the kernel sums in
+fp32, so the bar is fp32 accumulation error (1e-5 of the largest magnitude)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (M, I, J)
+    (25216, 384, 1152),   # DeiT-S QKV projection, batch 128
+    (25216, 1536, 384),   # DeiT-S FF Dense_1
+    (197, 768, 1000),     # ragged tokens, head-like J
+    (1000, 24, 40),       # tiny, I/J below one tile
+    (64, 8, 8),
+]
+
+
+@pytest.mark.parametrize("M,I,J", SHAPES)
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_dw(dev, M, I, J, bias):
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(M + I + J)
+    x = torch.randn(M, I, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, J, device=dev, generator=g).to(torch.bfloat16)
+    dw = torch.empty(I, J, device=dev)
+    db = torch.empty(J, device=dev) if bias else None
+    ops.gemm_dw(x, dy, dw, db)
+    ref = (x.double().t() @ dy.double())
+    err = float((dw.double() - ref).abs().max() / ref.abs().max())
+    assert err <= 1e-5, err
+    if bias:
+        rb = dy.double().sum(0)
+        assert float((db.double() - rb).abs().max() / rb.abs().max()) <= 1e-5
+
+
+def test_gemm_dw_accumulate_strided(dev):
+    """accumulate=True adds into an existing gradient; x / dy may be column slices of wider rows."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(7)
+    M, I, J = 3000, 128, 256
+    xw = torch.randn(M, I + 64, device=dev, generator=g).to(torch.bfloat16)
+    dyw = torch.randn(M, J + 8, device=dev, generator=g).to(torch.bfloat16)
+    x, dy = xw[:, 64:], dyw[:, :J]
+    dw0 = torch.randn(I, J, device=dev, generator=g)
+    db0 = torch.randn(J, device=dev, generator=g)
+    dw, db = dw0.clone(), db0.clone()
+    ops.gemm_dw(x, dy, dw, db, accumulate=True)
+    ref = dw0.double() + x.double().t() @ dy.double()
+    assert float((dw.double() - ref).abs().max() / ref.abs().max()) <= 1e-5
+    rb = db0.double() + dy.double().sum(0)
+    assert float((db.double() - rb).abs().max() / rb.abs().max()) <= 1e-5
+
+
+def test_gemm_dw_deterministic(dev):
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(25216, 384, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(25216, 384, device=dev, generator=g).to(torch.bfloat16)
+    a, b = torch.empty(384, 384, device=dev), torch.empty(384, 384, device=dev)
+    ops.gemm_dw(x, dy, a)
+    ops.gemm_dw(x, dy, b)
+    assert torch.equal(a, b)
+
+
+def test_dense_grads_match_autograd(dev):
+    """ops.dense (library fwd / dX, HIP dW / db) against float64 products of the same bf16 values."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(4, 197, 384, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(384, 1152, device=dev, generator=g) * 0.05).requires_grad_()
+    b = torch.randn(1152, device=dev, generator=g).requires_grad_()
+    dy = torch.randn(4, 197, 1152, device=dev, generator=g).to(torch.bfloat16)
+    y = ops.dense(x, w, b, torch.bfloat16)
+    y.backward(dy)
+    xd, wd = x.detach().double(), w.detach().to(torch.bfloat16).double()
+    ref_w = xd.reshape(-1, 384).t() @ dy.double().reshape(-1, 1152)
+    assert float((w.grad.double() - ref_w).abs().max() / ref_w.abs().max()) <= 1e-5
+    ref_b = dy.double().reshape(-1, 1152).sum(0)
+    assert float((b.grad.double() - ref_b).abs().max() / ref_b.abs().max()) <= 1e-5
+    ref_x = dy.double() @ wd.t()
+    assert float((x.grad.double() - ref_x).abs().max() / ref_x.abs().max()) <= 2e-2

@@ -1,0 +1,90 @@
+"""Residual add + LayerNorm kernels (sae_layernorm_fwd/bwd) and the fused ViT encoder path
+against the CPU oracle (oracle/vit_ref.py restating models/vit.py:9-99).
+
+LayerNorm statistics are fp32 in both; the output is bf16 (Flax nn.LayerNorm(dtype=bfloat16)),
+so y is checked at the bf16 bar (2e-2 of max|ref|); x + delta, dx and dscale / dbias are fp32
+sums of the same bf16 inputs and are checked at 1e-5."""
+import numpy as np
+import pytest
+
+import vit_ref
+from _util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,C", [(25216, 384), (1000, 768), (37, 192), (5, 1024), (3, 4)])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_add_layer_norm(dev, M, C, with_delta):
+    import torch
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(M + C)
+    x = (torch.randn(M, C, device=dev, generator=g) * 3 + 1).requires_grad_()
+    gamma = (torch.rand(C, device=dev, generator=g) + 0.5).requires_grad_()
+    beta = torch.randn(C, device=dev, generator=g).requires_grad_()
+    delta = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16).requires_grad_() if with_delta else None
+    dy = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
+    dxo = torch.randn(M, C, device=dev, generator=g) if with_delta else None
+    if with_delta:
+        xo, y = ops.add_layer_norm(x, delta, gamma, beta)
+        torch.autograd.backward([xo, y], [dxo, dy])
+    else:
+        y = ops.layer_norm(x, gamma, beta)
+        y.backward(dy)
+    xs = x.detach().double().cpu().numpy()
+    if with_delta:
+        xs = xs + delta.detach().double().cpu().numpy()
+        assert rel_err(xo, xs) <= 1e-6
+    s, b = gamma.detach().double().cpu().numpy(), beta.detach().double().cpu().numpy()
+    yr, cache = vit_ref.layer_norm(xs, s, b)
+    assert y.dtype == torch.bfloat16
+    assert rel_err(y.float(), yr) <= 2e-2
+    dx, ds, db = vit_ref.layer_norm_bwd(dy.double().cpu().numpy(), s, cache)
+    if with_delta:
+        dx = dx + dxo.double().cpu().numpy()
+        assert rel_err(delta.grad.float(), dx) <= 2e-2
+    assert rel_err(x.grad, dx) <= 1e-5
+    assert rel_err(gamma.grad, ds) <= 1e-5
+    assert rel_err(beta.grad, db) <= 1e-5
+
+
+def test_layer_norm_deterministic(dev):
+    import torch
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(25216, 384, device=dev, generator=g)
+    gamma, beta = torch.ones(384, device=dev), torch.zeros(384, device=dev)
+    dy = torch.randn(25216, 384, device=dev, generator=g).to(torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        xx, gg, bb = x.clone().requires_grad_(), gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+        ops.layer_norm(xx, gg, bb).backward(dy)
+        outs.append((xx.grad, gg.grad, bb.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_vit_train_grads_vs_oracle(dev):
+    """Whole bf16 ViT training step (patch GEMM, fused add+LayerNorm, fused attention, HIP weight
+    gradients, FF, head, smoothed CE) vs the fp64 numpy oracle with the same parameters."""
+    import torch
+    import sae_vision_amd.vit as vit
+    import sae_vision_amd.train as train
+    torch.manual_seed(0)
+    m = vit.ViT(num_classes=10, num_layers=2, num_heads=2, embed_dim=64, patch_shape=(8, 8), img_size=32,
+                dtype=torch.bfloat16, device=dev)
+    with torch.no_grad():
+        m.Dense_0.kernel.normal_(0, 0.1)
+    params = {k: v.detach().double().cpu().numpy() for k, v in m.named_parameters()}
+    rng = np.random.default_rng(0)
+    images = rng.standard_normal((4, 32, 32, 3))
+    labels = rng.integers(0, 10, size=4)
+    loss_ref, logits_ref, grads_ref = vit_ref.vit_loss_and_grads(params, images, labels, 2, 2, 8)
+    logits = m(torch.tensor(images, device=dev, dtype=torch.float32), is_training=True)
+    loss = train.smoothed_cross_entropy(logits, torch.tensor(labels, device=dev), 0.1)
+    loss.backward()
+    assert rel_err(logits.float(), logits_ref) <= 3e-2
+    assert abs(float(loss) - loss_ref) <= 3e-2 * abs(loss_ref)
+    for k, p in m.named_parameters():
+        err = rel_err(p.grad, grads_ref[k])
+        assert err <= 6e-2, f"{k}: rel err {err:.3e}"
