@@ -15,6 +15,7 @@
 #include "th_kernels.h"
 #include "variants.h"
 #include "fwd2.h"
+#include "fwd3.h"
 #include "bwd2.h"
 #include "gemm_dw.h"
 #include "ln.h"
@@ -167,6 +168,17 @@ template <int DP, int NW, int MINW, bool LSUM> int fwd2_run(hipStream_t st, cons
   return check_launch("attn_fwd2");
 }
 
+// bf16 forward with two 32-row query blocks per wave (fwd3.h): NW waves x 64 query rows
+template <int DP, int NW, int MINW, bool LSUM> int fwd3_run(hipStream_t st, const AttnArgs& a) {
+  const int nqb = (a.Nq + 64 * NW - 1) / (64 * NW);
+  const long long grid = (long long)nqb * a.H * a.B;
+  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  const size_t lds = std::max(4 * (size_t)F2<DP>::TILE, (size_t)2 * NW * 32 * DP * 2);
+  if (int rc = lds_attr((const void*)attn_fwd3_kernel<DP, NW, MINW, LSUM>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd3_kernel<DP, NW, MINW, LSUM>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
+  return check_launch("attn_fwd3");
+}
+
 // SAE_FWD_VARIANT (development A/B knob): "v1" = attn_fwd_kernel; default = fwd2 4 waves, MFMA row sum
 int fwd2_variant() {
   const char* e = getenv("SAE_FWD_VARIANT");
@@ -181,8 +193,12 @@ template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) 
     case 4: return fwd2_run<DP, 4, 2, true>(st, a);
     case 5: return fwd2_run<DP, 4, 3, true>(st, a);
     case 6: return fwd2_run<DP, 4, 3, false>(st, a);
-    default: return fwd2_run<DP, 4, 2, true>(st, a);
+    case 7: if constexpr (DP <= 64) return fwd3_run<DP, 4, 2, true>(st, a); else break;
+    case 8: if constexpr (DP <= 64) return fwd3_run<DP, 8, 1, true>(st, a); else break;
+    case 9: if constexpr (DP <= 64) return fwd3_run<DP, 4, 2, false>(st, a); else break;
+    default: break;
   }
+  return fwd2_run<DP, 4, 2, true>(st, a);
 }
 
 // lean bf16 backward (bwd2.h): dQ pass (publishes delta) then dK/dV pass
@@ -730,7 +746,7 @@ int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const 
 
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
   if (M < 1 || C < 1) return 0;
-  return (size_t)ln_bwd_blocks(M) * 2 * C * sizeof(float);
+  return ((size_t)ln_bwd_blocks(M) + kLnSplit) * 2 * C * sizeof(float);
 }
 
 int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
@@ -768,8 +784,13 @@ int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const 
     default: hipLaunchKernelGGL(ln_bwd_kernel<4>, g, b, 0, st, a); break;
   }
   if (int rc = check_launch("layernorm_bwd")) return rc;
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64), dim3(256), 0, st, a);
-  return check_launch("layernorm_bwd_reduce");
+  float* part2 = a.part + (size_t)a.nblk * 2 * C;
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
+                     (const float*)a.part, a.nblk, part2);
+  if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
+                     kLnSplit, (float*)nullptr);
+  return check_launch("layernorm_bwd_reduce2");
 }
 
 const char* sae_last_error(void) { return g_err.c_str(); }

@@ -174,26 +174,39 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
   }
 }
 
-// dgamma / dbeta = sum of the workgroup partials in workgroup order (deterministic):
-// 256 threads = 64 columns x 4 strided groups, then the 4 group sums in order.
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a) {
+// dgamma / dbeta = sum of the workgroup partials in workgroup order (deterministic), two levels
+// so that no thread walks a long dependent chain of loads: blockIdx.y = p of kLnSplit sums
+// partials [p*nblk/kLnSplit, (p+1)*nblk/kLnSplit) into part2[p] (256 threads = 64 columns x 4
+// strided groups, group sums in order); the final pass (gridDim.y == 1, nblk == kLnSplit, reading
+// part2) writes dgamma / dbeta.
+constexpr int kLnSplit = 16;
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a, const float* src, int nsrc, float* dst) {
   __shared__ float red[4][2][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
+  const int per = (nsrc + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * per, b1 = min(nsrc, b0 + per);
   float sg = 0.f, sb = 0.f;
   if (c < a.C) {
-#pragma unroll 8
-    for (int b = grp; b < a.nblk; b += 4) {
-      sg += a.part[((size_t)b * 2) * a.C + c];
-      sb += a.part[((size_t)b * 2 + 1) * a.C + c];
+#pragma unroll 4
+    for (int b = b0 + grp; b < b1; b += 4) {
+      sg += src[((size_t)b * 2) * a.C + c];
+      sb += src[((size_t)b * 2 + 1) * a.C + c];
     }
   }
   red[grp][0][cl] = sg;
   red[grp][1][cl] = sb;
   __syncthreads();
   if (grp == 0 && c < a.C) {
-    a.dgamma[c] = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-    a.dbeta[c] = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+    const float g = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+    const float bb = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+    if (dst) {
+      dst[((size_t)blockIdx.y * 2) * a.C + c] = g;
+      dst[((size_t)blockIdx.y * 2 + 1) * a.C + c] = bb;
+    } else {
+      a.dgamma[c] = g;
+      a.dbeta[c] = bb;
+    }
   }
 }
 

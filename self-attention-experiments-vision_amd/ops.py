@@ -388,9 +388,8 @@ class _Dense(torch.autograd.Function):
         I, J = w.shape
         wd = w.to(dt)
         x2 = x.to(dt).reshape(-1, I)
-        y = x2 @ wd
-        if b is not None:
-            y = y + b.to(dt)
+        # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
+        y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
         ctx.save_for_backward(x2, wd)
         ctx.has_b, ctx.xshape, ctx.wdtype, ctx.xdtype = b is not None, x.shape, w.dtype, x.dtype
         return y.view(*x.shape[:-1], J)

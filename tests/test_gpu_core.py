@@ -154,3 +154,33 @@ def test_error_reporting(dev):
     q = torch.zeros(1, 4, 1, 256, device=dev)
     with pytest.raises(SaeError, match="head_dim 256"):
         ops.attention(q, q, q)
+
+
+VARIANT_CASES = [
+    (2, 197, 197, 6, 64),      # DeiT-S layer: last wave of the workgroup partly / fully idle
+    (1, 577, 577, 2, 64),      # ViT-B/16@384
+    (1, 37, 37, 3, 64),        # ragged: second query block of the only wave is empty
+    (2, 100, 37, 3, 32),       # Nq != Nk, head dim 32
+    (1, 65, 129, 2, 48),       # tile boundaries + 1, padded head dim
+]
+
+
+@pytest.mark.parametrize("var", [2, 3, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("B,Nq,Nk,H,D", VARIANT_CASES)
+def test_fwd_variants(dev, monkeypatch, var, B, Nq, Nk, H, D):
+    """Every bf16 forward schedule selectable by SAE_FWD_VARIANT (fwd2 / fwd3 instances) matches
+    the oracle, output and log-sum-exp, so any of them can be promoted to the default."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    monkeypatch.setenv("SAE_FWD_VARIANT", str(var))
+    rng = np.random.default_rng(var)
+    q, k, v = (randn(rng, (B, n, H, D), "bf16") for n in (Nq, Nk, Nk))
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=torch.bfloat16) for x in (q, k, v))
+    o, lse = ops._fwd(tq, tk, tv, 1.0 / math.sqrt(D))
+    torch.cuda.synchronize()
+    assert rel_err(o, R.attention_core_fwd(q, k, v, "bf16")) <= TOL["bf16"]
+    s = np.einsum("bqhd,bkhd->bhqk", q.astype(np.float64), k.astype(np.float64)) / math.sqrt(D)
+    mx = s.max(-1, keepdims=True)
+    lse_ref = (mx + np.log(np.exp(s - mx).sum(-1, keepdims=True)))[..., 0]
+    assert np.abs(lse.float().cpu().numpy() - lse_ref).max() <= 1e-3 * max(1.0, np.abs(lse_ref).max())

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--shapes", default="deit_s,vitb384,cait_s24,cait_ca,bot14,bot7")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B")
+    ap.add_argument("--bwd-variants", default="", help="comma list of SAE_BWD_VARIANT values to A/B")
     args = ap.parse_args()
     import torch
     import sae_vision_amd.ops as ops
@@ -42,8 +44,13 @@ def main():
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     elt = 2 if args.dtype == "bf16" else 4
     results = {}
-    for name in args.shapes.split(","):
-        B, Nq, Nk, H, D = SHAPES[name]
+    fv = args.fwd_variants.split(",") if args.fwd_variants else [os.environ.get("SAE_FWD_VARIANT", "")]
+    bv = args.bwd_variants.split(",") if args.bwd_variants else [os.environ.get("SAE_BWD_VARIANT", "")]
+    runs = [(n, f, b) for n in args.shapes.split(",") for f in fv for b in bv]
+    for shape, fvar, bvar in runs:
+        os.environ["SAE_FWD_VARIANT"], os.environ["SAE_BWD_VARIANT"] = fvar, bvar
+        name = shape + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
+        B, Nq, Nk, H, D = SHAPES[shape]
         g = torch.Generator(device=dev).manual_seed(0)
         q = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
         k = torch.randn(B, Nk, H, D, device=dev, generator=g).to(dt)
@@ -92,7 +99,7 @@ def main():
              "fwdbwd_tflops": round((ff + fb) / (mf + mb) / 1e12, 1),
              "fwd_gbs": round(bf / mf / 1e9), "bwd_gbs": round(bb / mb / 1e9)}
         results[name] = r
-        print(f"{name:12s} B={B:4d} Nq={Nq:5d} Nk={Nk:5d} H={H:3d} D={D:4d} | fwd {r['fwd_us']:8.1f} us "
+        print(f"{name:16s} B={B:4d} Nq={Nq:5d} Nk={Nk:5d} H={H:3d} D={D:4d} | fwd {r['fwd_us']:8.1f} us "
               f"{r['fwd_tflops']:7.1f} TF {r['fwd_gbs']:6d} GB/s | bwd {r['bwd_us']:8.1f} us {r['bwd_tflops']:7.1f} TF "
               f"{r['bwd_gbs']:6d} GB/s | fwd+bwd {r['fwdbwd_tflops']:7.1f} TF", flush=True)
     if args.json:

@@ -1,9 +1,17 @@
 #!/usr/bin/env python3
-"""Probe library GEMM (torch.matmul -> hipBLASLt) throughput at the DeiT-S / ViT-B training shapes.
+"""Projection GEMM throughput at the DeiT-S / ViT-B training shapes: the library GEMM
+(torch.matmul -> hipBLASLt) for y = x W, dX = dY W^T, dW = X^T dY, next to this repo's
+split-token weight-gradient kernel (sae_gemm_dw, fp32 out + fused bias sum).
 
     python tools/gemm_probe.py
 """
+import os
+import sys
+
 import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def bench(fn, iters=20):
@@ -20,24 +28,27 @@ def bench(fn, iters=20):
 
 
 def main():
+    import sae_vision_amd.ops as ops
     dev = torch.device("cuda:0")
     M = 128 * 197
     shapes = [  # (name, M, K, N)
-        ("qkv_fwd", M, 384, 1152), ("oproj_fwd", M, 384, 384), ("ff1_fwd", M, 384, 1536), ("ff2_fwd", M, 1536, 384),
-        ("square8k", 8192, 8192, 8192), ("square4k", 4096, 4096, 4096),
-        ("b384_ff1", 32 * 577, 768, 3072), ("b384_ff2", 32 * 577, 3072, 768),
+        ("qkv", M, 384, 1152), ("oproj", M, 384, 384), ("ff1", M, 384, 1536), ("ff2", M, 1536, 384),
+        ("b384_qkv", 32 * 577, 768, 2304), ("b384_ff1", 32 * 577, 768, 3072), ("b384_ff2", 32 * 577, 3072, 768),
     ]
     for name, m, k, n in shapes:
         a = torch.randn(m, k, device=dev).to(torch.bfloat16)
         b = torch.randn(k, n, device=dev).to(torch.bfloat16)
-        ms = bench(lambda: a @ b)
-        # weight gradient orientation: a^T @ dy  ([k, m] x [m, n])
         dy = torch.randn(m, n, device=dev).to(torch.bfloat16)
-        ms_w = bench(lambda: a.t() @ dy)
+        dw = torch.empty(k, n, device=dev)
+        db = torch.empty(n, device=dev)
+        ms = bench(lambda: a @ b)
         ms_x = bench(lambda: dy @ b.t())
+        ms_w = bench(lambda: a.t() @ dy)
+        ms_h = bench(lambda: ops.gemm_dw(a, dy, dw, db))
         f = 2.0 * m * n * k
-        print(f"{name:10s} M={m:6d} K={k:5d} N={n:5d}  fwd {ms*1e3:8.1f} us {f/ms/1e9:7.1f} TF | "
-              f"dW {ms_w*1e3:8.1f} us {f/ms_w/1e9:7.1f} TF | dX {ms_x*1e3:8.1f} us {f/ms_x/1e9:7.1f} TF", flush=True)
+        print(f"{name:9s} M={m:6d} K={k:5d} N={n:5d} | fwd {ms*1e3:7.1f} us {f/ms/1e9:7.1f} TF | dX {ms_x*1e3:7.1f} us "
+              f"{f/ms_x/1e9:7.1f} TF | dW lib {ms_w*1e3:7.1f} us {f/ms_w/1e9:7.1f} TF | dW+db hip {ms_h*1e3:7.1f} us "
+              f"{f/ms_h/1e9:7.1f} TF", flush=True)
 
 
 if __name__ == "__main__":
