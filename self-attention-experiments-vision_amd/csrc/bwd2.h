@@ -43,14 +43,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   const __bf16* O = reinterpret_cast<const __bf16*>(a.o) + b * a.os[0] + hh * a.os[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
 
-  F2Stage<DP, NW> kst, vst;
-  kst.init(tid, a.ks[1], a.D);
-  vst.init(tid, a.vs[1], a.D);
+  F2Stage<DP, NW> kst[2], vst[2];   // two register stages in flight (as in fwd2.h)
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    kst[r].init(tid, a.ks[1], a.D);
+    vst[r].init(tid, a.vs[1], a.D);
+  }
   const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
   const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
   const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
-  kst.load(rk, 0);
-  vst.load(rv, 0);
+  const int nkt = (a.Nk + 63) / 64;
+  kst[0].load(rk, 0);
+  vst[0].load(rv, 0);
+  if (nkt > 1) {
+    kst[1].load(rk, kstep);
+    vst[1].load(rv, vstep);
+  }
 
   bf16x8 qf[NS], gf[NS];
   float dlt;
@@ -97,10 +105,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   f32x16 adq[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) adq[t] = zero16();
-  const int nkt = (a.Nk + 63) / 64;
 
-  kst.write(smem);
-  vst.write(smem + TILE);
+  kst[0].write(smem);
+  vst[0].write(smem + TILE);
+  vm_wait_all();   // Q / dO fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   for (int kt = 0; kt < nkt; kt += 2) {
 #pragma unroll
@@ -110,10 +118,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       const char* ldsK = smem + bsel * 2 * TILE;
       const char* ldsV = ldsK + TILE;
       char* nxt = smem + (bsel ^ 1) * 2 * TILE;
-      const bool more = t + 1 < nkt;
-      if (more) {
-        kst.load(rk, (unsigned)(t + 1) * kstep);
-        vst.load(rv, (unsigned)(t + 1) * vstep);
+      if (t + 2 < nkt) {   // register set bsel went to LDS at the end of tile t - 1
+        kst[bsel].load(rk, (unsigned)(t + 2) * kstep);
+        vst[bsel].load(rv, (unsigned)(t + 2) * vstep);
       }
       const int nvalid = min(64, a.Nk - 64 * t);
       if (active) {
@@ -153,9 +160,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
           }
         }
       }
-      if (more) {
-        kst.write(nxt);
-        vst.write(nxt + TILE);
+      if (t + 1 < nkt) {
+        kst[bsel ^ 1].write(nxt);
+        vst[bsel ^ 1].write(nxt + TILE);
       }
       __syncthreads();
     }
@@ -196,23 +203,29 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
 
-  F2Stage<DP, NW> qst, gst;
-  qst.init(tid, a.qs[1], a.D);
-  gst.init(tid, a.dos[1], a.D);
+  // Q / dO tiles and their row constants: two register stages in flight (as in fwd2.h)
+  F2Stage<DP, NW> qst[2], gst[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    qst[r].init(tid, a.qs[1], a.D);
+    gst[r].init(tid, a.dos[1], a.D);
+  }
   const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
   const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
   const unsigned qstep = (unsigned)(64 * a.qs[1] * 2), gstep = (unsigned)(64 * a.dos[1] * 2);
-  qst.load(rq, 0);
-  gst.load(rg, 0);
-  float rc_l = 0.f, rc_d = 0.f;   // row constants of the staged tile (threads 0..63)
-  auto fetch_rc = [&](int qt) {
+  const int nqt = (a.Nq + 63) / 64;
+  float rc_l[2] = {0.f, 0.f}, rc_d[2] = {0.f, 0.f};   // row constants of a staged tile (threads 0..63)
+  auto fetch = [&](int r, int qt) {
+    qst[r].load(rq, (unsigned)qt * qstep);
+    gst[r].load(rg, (unsigned)qt * gstep);
     if (tid < 64) {
       const int qq = qt * 64 + tid;
-      rc_l = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
-      rc_d = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+      rc_l[r] = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
+      rc_d[r] = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
     }
   };
-  fetch_rc(0);
+  fetch(0, 0);
+  if (nqt > 1) fetch(1, 1);
 
   bf16x8 kf[NS], vf[NS];
   {
@@ -251,16 +264,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     adk[t] = zero16();
     adv[t] = zero16();
   }
-  const int nqt = (a.Nq + 63) / 64;
-  auto put = [&](char* buf) {
-    qst.write(buf);
-    gst.write(buf + TILE);
+  auto put = [&](int r, char* buf) {
+    qst[r].write(buf);
+    gst[r].write(buf + TILE);
     if (tid < 64) {
-      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = rc_l;
-      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d;
+      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = rc_l[r];
+      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d[r];
     }
   };
-  put(smem);
+  put(0, smem);
+  vm_wait_all();   // K / V fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
 #pragma unroll
@@ -272,12 +285,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
       const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
       const float* ldsD = ldsL + 64;
       char* nxt = smem + (bsel ^ 1) * TB;
-      const bool more = qt + 1 < nqt;
-      if (more) {
-        qst.load(rq, (unsigned)(qt + 1) * qstep);
-        gst.load(rg, (unsigned)(qt + 1) * gstep);
-        fetch_rc(qt + 1);
-      }
+      if (qt + 2 < nqt) fetch(bsel, qt + 2);   // register set bsel went to LDS at the end of tile qt - 1
       if (active) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
           }
         }
       }
-      if (more) put(nxt);
+      if (qt + 1 < nqt) put(bsel ^ 1, nxt);
       __syncthreads();
     }
   }

@@ -56,6 +56,12 @@ template <> struct MF<float> {
 
 __device__ __forceinline__ f32x16 zero16() { return f32x16{}; }
 
+// s_waitcnt vmcnt(0) as a real S_WAITCNT (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait).  Put it
+// after prologue loads whose registers stay live through a loop: otherwise the waitcnt pass,
+// seeing them possibly outstanding at the loop header, waits at their first use INSIDE the loop
+// with counts that, from the second trip on, drain the loop's own prefetch every iteration.
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ------------------------------------------------------------------------------ LDS images
 // bf16 tiles are [rows][DP] with 16-byte chunks XOR-swizzled per row so that both the
 // ds_read_b128 row reads (MFMA row operand) and the ds_read_b64_tr_b16 column reads

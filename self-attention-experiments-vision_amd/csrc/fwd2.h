@@ -14,8 +14,8 @@
 //   * lazy rescale (T13, threshold 2^8) decided wave-uniformly before any P of the tile is
 //     exponentiated, as in the v1 kernel.
 // One wave owns 32 query rows (query on the MFMA lane, "swapped" S^T = K Q^T), NW waves share
-// each 64-key K/V tile staged global -> registers -> LDS (issue early, write late; one
-// barrier per tile).
+// each 64-key K/V tile staged global -> registers -> LDS (issued two tiles ahead, written one
+// tile ahead; one barrier per tile).
 #pragma once
 #include "common.h"
 
@@ -196,14 +196,24 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
 
   wg_stamp(a.dbgbuf, a.dbg, 0);
   if (a.dbg & 4) return;
-  F2Stage<DP, NW> kst, vst;
-  kst.init(tid, a.ks[1], a.D);
-  vst.init(tid, a.vs[1], a.D);
+  // K/V tiles: two register stages in flight (tile t + 2 is loaded while tile t computes and
+  // tile t + 1, loaded one tile earlier, is written to LDS at its end)
+  F2Stage<DP, NW> kst[2], vst[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    kst[r].init(tid, a.ks[1], a.D);
+    vst[r].init(tid, a.vs[1], a.D);
+  }
   const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
   const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
   const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
-  kst.load(rk, 0);
-  vst.load(rv, 0);
+  const int nkt = (a.Nk + 63) / 64;
+  kst[0].load(rk, 0);
+  vst[0].load(rv, 0);
+  if (nkt > 1) {
+    kst[1].load(rk, kstep);
+    vst[1].load(rv, vstep);
+  }
 
   // query fragments (row q, head-dim 16s + 8h .. +7), zero past Nq / D
   bf16x8 qf[NS];
@@ -238,10 +248,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   f32x16 lacc = zero16();
   float m = -kInf, l = 0.f;
   const float sl2 = a.scale * kLog2e;
-  const int nkt = (a.Nk + 63) / 64;
 
-  kst.write(smem);
-  vst.write(smem + TILE);
+  kst[0].write(smem);
+  vst[0].write(smem + TILE);
+  vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   wg_stamp(a.dbgbuf, a.dbg, 1);
   // two tiles per trip: buffer 0 then buffer 1 (immediate LDS offsets)
@@ -252,16 +262,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       if (t >= nkt) break;
       char* cur = smem + bsel * 2 * TILE;
       char* nxt = smem + (bsel ^ 1) * 2 * TILE;
-      const bool more = t + 1 < nkt;
-      if (more && !(a.dbg & 1)) {
-        kst.load(rk, (unsigned)(t + 1) * kstep);
-        vst.load(rv, (unsigned)(t + 1) * vstep);
+      if (t + 2 < nkt && !(a.dbg & 1)) {   // register set bsel went to LDS at the end of tile t - 1
+        kst[bsel].load(rk, (unsigned)(t + 2) * kstep);
+        vst[bsel].load(rv, (unsigned)(t + 2) * vstep);
       }
       if (active && !(a.dbg & 2))
         fwd2_tile<DP, NW, LSUM>(cur, cur + TILE, qf, acco, lacc, m, l, min(64, a.Nk - 64 * t), sl2, ka, va, h);
-      if (more) {
-        kst.write(nxt);
-        vst.write(nxt + TILE);
+      if (t + 1 < nkt) {
+        kst[bsel ^ 1].write(nxt);
+        vst[bsel ^ 1].write(nxt + TILE);
       }
       __syncthreads();
     }

@@ -139,14 +139,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd3_kernel(AttnArgs a) {
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
 
-  F2Stage<DP, NW> kst, vst;
-  kst.init(tid, a.ks[1], a.D);
-  vst.init(tid, a.vs[1], a.D);
+  F2Stage<DP, NW> kst[2], vst[2];   // two register stages in flight, as in fwd2
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    kst[r].init(tid, a.ks[1], a.D);
+    vst[r].init(tid, a.vs[1], a.D);
+  }
   const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
   const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
   const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
-  kst.load(rk, 0);
-  vst.load(rv, 0);
+  const int nkt = (a.Nk + 63) / 64;
+  kst[0].load(rk, 0);
+  vst[0].load(rv, 0);
+  if (nkt > 1) {
+    kst[1].load(rk, kstep);
+    vst[1].load(rv, vstep);
+  }
 
   bf16x8 qf[2][NS];
   {
@@ -185,10 +193,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd3_kernel(AttnArgs a) {
   }
   float m[2] = {-kInf, -kInf}, l[2] = {0.f, 0.f};
   const float sl2 = a.scale * kLog2e;
-  const int nkt = (a.Nk + 63) / 64;
 
-  kst.write(smem);
-  vst.write(smem + TILE);
+  kst[0].write(smem);
+  vst[0].write(smem + TILE);
+  vm_wait_all();
   __syncthreads();
   for (int kt = 0; kt < nkt; kt += 2) {
 #pragma unroll
@@ -197,16 +205,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd3_kernel(AttnArgs a) {
       if (t >= nkt) break;
       char* cur = smem + bsel * 2 * TILE;
       char* nxt = smem + (bsel ^ 1) * 2 * TILE;
-      const bool more = t + 1 < nkt;
-      if (more) {
-        kst.load(rk, (unsigned)(t + 1) * kstep);
-        vst.load(rv, (unsigned)(t + 1) * vstep);
+      if (t + 2 < nkt) {
+        kst[bsel].load(rk, (unsigned)(t + 2) * kstep);
+        vst[bsel].load(rv, (unsigned)(t + 2) * vstep);
       }
       if (active)
         fwd3_tile<DP, LSUM>(cur, cur + TILE, qf, acco, lacc, m, l, min(64, a.Nk - 64 * t), sl2, ka, va, h);
-      if (more) {
-        kst.write(nxt);
-        vst.write(nxt + TILE);
+      if (t + 1 < nkt) {
+        kst[bsel ^ 1].write(nxt);
+        vst[bsel ^ 1].write(nxt + TILE);
       }
       __syncthreads();
     }

@@ -11,7 +11,8 @@
 //   * a workgroup owns a 128 x 128 output tile and one contiguous chunk of tokens; 4 waves,
 //     each a 64 x 64 quarter (2 x 2 accumulators of v_mfma_f32_32x32x16_bf16);
 //   * X and dY chunks of 64 tokens are staged global -> registers -> LDS as [token][column]
-//     images (XOR-swizzled 256-byte rows), double-buffered, and both MFMA operands are read
+//     images (XOR-swizzled 256-byte rows), double-buffered in LDS with two register stages in
+//     flight (loads issued two stages ahead of use), and both MFMA operands are read
 //     with ds_read_b64_tr_b16 (K = tokens on the transposed axis, same permuted K order on both);
 //   * db rides on the matrix pipe: an all-ones A operand times the dY fragment gives column sums;
 //   * each split writes an fp32 partial tile; a second kernel sums the splits in a fixed order
@@ -76,11 +77,13 @@ template <bool BIAS>
 __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int IMG = kDwK * 256;     // 16 KiB per operand image
-  const int ti = (a.I + kDwT - 1) / kDwT;
-  int bid = blockIdx.x;
-  const int s = bid % a.S;            // consecutive blocks = splits of one tile
-  bid /= a.S;
-  const int it = bid % ti, jt = bid / ti;
+  const int ti = (a.I + kDwT - 1) / kDwT, tj = (a.J + kDwT - 1) / kDwT;
+  // XCD-aware order: the logical blocks of one XCD are a contiguous range, tiles fastest, so
+  // every tile of a token chunk runs on the same XCD at the same time and the chunk's X / dY
+  // rows are fetched from HBM once per XCD (L2 hits for the other tiles), not once per tile
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ti * tj), s = bid / (ti * tj);
+  const int it = tile % ti, jt = tile / ti;
   const int i0 = it * kDwT, j0 = jt * kDwT;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,12 +95,22 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   // row ranges [m0, m1) of X and dY through buffer descriptors (rows past m1 read zero)
   const __amdgpu_buffer_rsrc_t rx = row_rsrc(a.x + (long long)m0 * a.ldx, m1 - m0, a.ldx);
   const __amdgpu_buffer_rsrc_t ry = row_rsrc(a.dy + (long long)m0 * a.ldy, m1 - m0, a.ldy);
-  DwStage<4> xs, ys;
-  xs.init(tid, a.ldx, i0, a.I);
-  ys.init(tid, a.ldy, j0, a.J);
+  // two register stages in flight: the loads for stage st + 2 are issued while stage st computes
+  // and stage st + 1 (issued one stage earlier) is written to LDS at its end
+  DwStage<4> xs[2], ys[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    xs[r].init(tid, a.ldx, i0, a.I);
+    ys[r].init(tid, a.ldy, j0, a.J);
+  }
   const unsigned xstep = (unsigned)(kDwK * a.ldx * 2), ystep = (unsigned)(kDwK * a.ldy * 2);
-  xs.load(rx, 0);
-  ys.load(ry, 0);
+  const int nst = (m1 - m0 + kDwK - 1) / kDwK;
+  xs[0].load(rx, 0);
+  ys[0].load(ry, 0);
+  if (nst > 1) {
+    xs[1].load(rx, xstep);
+    ys[1].load(ry, ystep);
+  }
 
   unsigned ca[8];   // [operand x / dy][t = 0, 1][r1, r2] transposed-read addresses
   {
@@ -126,9 +139,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
-  const int nst = (m1 - m0 + kDwK - 1) / kDwK;
-  xs.write(smem);
-  ys.write(smem + IMG);
+  xs[0].write(smem);
+  ys[0].write(smem + IMG);
   __syncthreads();
   for (int st0 = 0; st0 < nst; st0 += 2) {
 #pragma unroll
@@ -138,10 +150,9 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
       const char* imx = smem + bsel * 2 * IMG;
       const char* imy = imx + IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
-      const bool more = st + 1 < nst;
-      if (more) {
-        xs.load(rx, (unsigned)(st + 1) * xstep);
-        ys.load(ry, (unsigned)(st + 1) * ystep);
+      if (st + 2 < nst) {   // register set bsel was written to LDS at the end of stage st - 1
+        xs[bsel].load(rx, (unsigned)(st + 2) * xstep);
+        ys[bsel].load(ry, (unsigned)(st + 2) * ystep);
       }
 #pragma unroll
       for (int k = 0; k < kDwK / 16; ++k) {
@@ -156,9 +167,9 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
           accb[1] = MF<__bf16>::mma(ones, b1, accb[1]);
         }
       }
-      if (more) {
-        xs.write(nxt);
-        ys.write(nxt + IMG);
+      if (st + 1 < nst) {
+        xs[bsel ^ 1].write(nxt);
+        ys[bsel ^ 1].write(nxt + IMG);
       }
       __syncthreads();
     }

@@ -81,3 +81,4 @@ def test_dense_grads_match_autograd(dev):
     assert float((b.grad.double() - ref_b).abs().max() / ref_b.abs().max()) <= 1e-5
     ref_x = dy.double() @ wd.t()
     assert float((x.grad.double() - ref_x).abs().max() / ref_x.abs().max()) <= 2e-2
+
