@@ -43,22 +43,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   const __bf16* O = reinterpret_cast<const __bf16*>(a.o) + b * a.os[0] + hh * a.os[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
 
-  F2Stage<DP, NW> kst[2], vst[2];   // two register stages in flight (as in fwd2.h)
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    kst[r].init(tid, a.ks[1], a.D);
-    vst[r].init(tid, a.vs[1], a.D);
-  }
+  F2Stage<DP, NW> kst, vst;   // K/V tile t + 1 loaded while tile t computes
+  kst.init(tid, a.ks[1], a.D);
+  vst.init(tid, a.vs[1], a.D);
   const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
   const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
   const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
   const int nkt = (a.Nk + 63) / 64;
-  kst[0].load(rk, 0);
-  vst[0].load(rv, 0);
-  if (nkt > 1) {
-    kst[1].load(rk, kstep);
-    vst[1].load(rv, vstep);
-  }
+  kst.load(rk, 0);
+  vst.load(rv, 0);
 
   bf16x8 qf[NS], gf[NS];
   float dlt;
@@ -102,71 +95,95 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
     }
   }
 
-  f32x16 adq[NT];
+  // -delta as the initial dP^T accumulator, made by one MFMA: ones (k = 0, 1) times the
+  // bf16 hi / lo split of -delta (k = 0, 1 of this lane's query column); dS = P o dP' then
+  // needs one multiply per element instead of a subtract and a multiply
+  bf16x8 dl_b, dl_a;
+  {
+    const __bf16 hi = (__bf16)(-dlt);
+    const __bf16 lo = (__bf16)(-dlt - (float)hi);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) adq[t] = zero16();
+    for (int j = 0; j < 8; ++j) {
+      dl_b[j] = (__bf16)0.f;
+      dl_a[j] = (__bf16)0.f;
+    }
+    if (h == 0) {
+      dl_b[0] = hi;
+      dl_b[1] = lo;
+      dl_a[0] = dl_a[1] = (__bf16)1.f;
+    }
+  }
+  f32x16 adq[NT];   // written first by the peeled first tile (zero C operand)
 
-  kst[0].write(smem);
-  vst[0].write(smem + TILE);
+  kst.write(smem);
+  vst.write(smem + TILE);
   vm_wait_all();   // Q / dO fragments resident before the loop (see vm_wait_all)
   __syncthreads();
-  for (int kt = 0; kt < nkt; kt += 2) {
+  // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1, barrier (as fwd2.h)
+  auto step = [&](int t, auto bsel_c, auto first_c, auto compute_c) {
+    constexpr int bsel = decltype(bsel_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+    const char* ldsK = smem + bsel * 2 * TILE;
+    const char* ldsV = ldsK + TILE;
+    char* nxt = smem + (bsel ^ 1) * 2 * TILE;
+    if (t + 1 < nkt) {
+      kst.load(rk, (unsigned)(t + 1) * kstep);
+      vst.load(rv, (unsigned)(t + 1) * vstep);
+    }
+    const int nvalid = min(64, a.Nk - 64 * t);
+    if constexpr (decltype(compute_c)::value) {
 #pragma unroll
-    for (int bsel = 0; bsel < 2; ++bsel) {
-      const int t = kt + bsel;
-      if (t >= nkt) break;
-      const char* ldsK = smem + bsel * 2 * TILE;
-      const char* ldsV = ldsK + TILE;
-      char* nxt = smem + (bsel ^ 1) * 2 * TILE;
-      if (t + 2 < nkt) {   // register set bsel went to LDS at the end of tile t - 1
-        kst[bsel].load(rk, (unsigned)(t + 2) * kstep);
-        vst[bsel].load(rv, (unsigned)(t + 2) * vstep);
-      }
-      const int nvalid = min(64, a.Nk - 64 * t);
-      if (active) {
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && nvalid <= 32) break;
+        f32x16 sp = zero16();
+        f32x16 dp = MF<__bf16>::mma(dl_a, dl_b, zero16());
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (u == 1 && nvalid <= 32) break;
-          f32x16 sp = zero16(), dp = zero16();
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 kr = *reinterpret_cast<const bf16x8*>(ldsK + ka[s] + 32 * u * DP * 2);
+          const bf16x8 vr = *reinterpret_cast<const bf16x8*>(ldsV + ka[s] + 32 * u * DP * 2);
+          sp = MF<__bf16>::mma(kr, qf[s], sp);
+          dp = MF<__bf16>::mma(vr, gf[s], dp);
+        }
+        if (nvalid < 64) {   // tail: keys past the end contribute nothing
+          const int nvh = nvalid - 32 * u - 4 * h;
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bf16x8 kr = *reinterpret_cast<const bf16x8*>(ldsK + ka[s] + 32 * u * DP * 2);
-            const bf16x8 vr = *reinterpret_cast<const bf16x8*>(ldsV + ka[s] + 32 * u * DP * 2);
-            sp = MF<__bf16>::mma(kr, qf[s], sp);
-            dp = MF<__bf16>::mma(vr, gf[s], dp);
-          }
-          if (nvalid < 64) {   // tail: keys past the end contribute nothing
-            const int nvh = nvalid - 32 * u - 4 * h;
+          for (int r = 0; r < 16; ++r) sp[r] = ((r & 3) + 8 * (r >> 2)) < nvh ? sp[r] : -kInf;
+        }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sp[r] = ((r & 3) + 8 * (r >> 2)) < nvh ? sp[r] : -kInf;
-          }
+        for (int r = 0; r < 16; ++r) dp[r] *= ex2(__builtin_fmaf(sp[r], sl2, lsc2));
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = ex2(__builtin_fmaf(sp[r], sl2, lsc2));
-            dp[r] = p * (dp[r] - dlt);
-          }
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 sf = acc_frag<__bf16>(dp, s2);
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x8 sf = acc_frag<__bf16>(dp, s2);
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-              const int ro = (32 * u + 16 * s2) * DP * 2;
-              s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt] + ro));
-              s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt + 1] + ro));
-              typedef __attribute__((ext_vector_type(8))) short s16x8;
-              s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
-              adq[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), sf, adq[tt]);
-            }
+          for (int tt = 0; tt < NT; ++tt) {
+            const int ro = (32 * u + 16 * s2) * DP * 2;
+            s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt] + ro));
+            s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsK + ca[2 * tt + 1] + ro));
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+            adq[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), sf,
+                                      (FIRST && u == 0 && s2 == 0) ? zero16() : adq[tt]);
           }
         }
       }
-      if (t + 1 < nkt) {
-        kst[bsel ^ 1].write(nxt);
-        vst[bsel ^ 1].write(nxt + TILE);
-      }
-      __syncthreads();
     }
-  }
+    if (t + 1 < nkt) {
+      kst.write(nxt);
+      vst.write(nxt + TILE);
+    }
+    __syncthreads();
+  };
+  auto sweep = [&](auto compute_c) {
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    step(0, B0{}, std::true_type{}, compute_c);
+    for (int t = 1; t < nkt; t += 2) {
+      step(t, B1{}, std::false_type{}, compute_c);
+      if (t + 1 < nkt) step(t + 1, B0{}, std::false_type{}, compute_c);
+    }
+  };
+  if (active) sweep(std::true_type{});   // waves past the last query row only stage and sync
+  else sweep(std::false_type{});
   if (active) {
     const int q0 = qb * BQ + w * 32;
     __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
@@ -258,12 +275,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     }
   }
 
-  f32x16 adk[NT], adv[NT];
+  f32x16 adk[NT], adv[NT];   // written first by the peeled first tile (zero C operand)
+  // -delta as the initial dP accumulator (one MFMA, as in the dQ pass): A = bf16 hi / lo split
+  // of -delta of this lane's query row at k = 0, 1, B = ones at k = 0, 1
+  bf16x8 one01;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    adk[t] = zero16();
-    adv[t] = zero16();
-  }
+  for (int j = 0; j < 8; ++j) one01[j] = (__bf16)((h == 0 && j < 2) ? 1.f : 0.f);
   auto put = [&](int r, char* buf) {
     qst[r].write(buf);
     gst[r].write(buf + TILE);
@@ -275,65 +292,86 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   put(0, smem);
   vm_wait_all();   // K / V fragments resident before the loop (see vm_wait_all)
   __syncthreads();
-  for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
+  auto step = [&](int qt, auto bsel_c, auto first_c, auto compute_c) {
+    constexpr int bsel = decltype(bsel_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+    const char* ldsQ = smem + bsel * TB;
+    const char* ldsG = ldsQ + TILE;
+    const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
+    const float* ldsD = ldsL + 64;
+    char* nxt = smem + (bsel ^ 1) * TB;
+    if (qt + 2 < nqt) fetch(bsel, qt + 2);   // register set bsel went to LDS at the end of tile qt - 1
+    if constexpr (decltype(compute_c)::value) {
 #pragma unroll
-    for (int bsel = 0; bsel < 2; ++bsel) {
-      const int qt = qt0 + bsel;
-      if (qt >= nqt) break;
-      const char* ldsQ = smem + bsel * TB;
-      const char* ldsG = ldsQ + TILE;
-      const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
-      const float* ldsD = ldsL + 64;
-      char* nxt = smem + (bsel ^ 1) * TB;
-      if (qt + 2 < nqt) fetch(bsel, qt + 2);   // register set bsel went to LDS at the end of tile qt - 1
-      if (active) {
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && qt * 64 + 32 >= a.Nq) break;
+        bf16x8 dla;
+        {
+          const float nd = -ldsD[32 * u + r32];
+          const __bf16 hi = (__bf16)nd;
+          const __bf16 lo = (__bf16)(nd - (float)hi);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (u == 1 && qt * 64 + 32 >= a.Nq) break;
-          f32x16 sp = zero16(), dp = zero16();
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bf16x8 qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
-            const bf16x8 gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
-            sp = MF<__bf16>::mma(qr, kf[s], sp);
-            dp = MF<__bf16>::mma(gr, vf[s], dp);
+          for (int j = 0; j < 8; ++j) dla[j] = (__bf16)0.f;
+          if (h == 0) {
+            dla[0] = hi;
+            dla[1] = lo;
           }
-          // rows q = 32u + row_of(r, h): constants for r = 4g + j at 32u + 8g + 4h + j
+        }
+        f32x16 sp = zero16();
+        f32x16 dp = MF<__bf16>::mma(dla, one01, zero16());
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
-            const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
+          const bf16x8 gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+          sp = MF<__bf16>::mma(qr, kf[s], sp);
+          dp = MF<__bf16>::mma(gr, vf[s], dp);
+        }
+        // rows q = 32u + row_of(r, h): constants for r = 4g + j at 32u + 8g + 4h + j
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float p = ex2(__builtin_fmaf(sp[4 * g + j], sl2, -l4[j]));
-              sp[4 * g + j] = p;
-              dp[4 * g + j] = p * (dp[4 * g + j] - d4[j]);
-            }
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float p = ex2(__builtin_fmaf(sp[4 * g + j], sl2, -l4[j]));
+            sp[4 * g + j] = p;
+            dp[4 * g + j] *= p;
           }
+        }
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x8 pf = acc_frag<__bf16>(sp, s2);
-            const bf16x8 sf = acc_frag<__bf16>(dp, s2);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = acc_frag<__bf16>(sp, s2);
+          const bf16x8 sf = acc_frag<__bf16>(dp, s2);
+          const bool z = FIRST && u == 0 && s2 == 0;
 #pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-              const int ro = (32 * u + 16 * s2) * DP * 2;
-              typedef __attribute__((ext_vector_type(8))) short s16x8;
-              s16x4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt] + ro));
-              s16x4 g2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt + 1] + ro));
-              s16x8 gv = {g1[0], g1[1], g1[2], g1[3], g2[0], g2[1], g2[2], g2[3]};
-              adv[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, gv), pf, adv[tt]);
-              s16x4 q1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt] + ro));
-              s16x4 q2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt + 1] + ro));
-              s16x8 qv = {q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
-              adk[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, qv), sf, adk[tt]);
-            }
+          for (int tt = 0; tt < NT; ++tt) {
+            const int ro = (32 * u + 16 * s2) * DP * 2;
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt] + ro));
+            s16x4 g2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsG + ca[2 * tt + 1] + ro));
+            s16x8 gv = {g1[0], g1[1], g1[2], g1[3], g2[0], g2[1], g2[2], g2[3]};
+            adv[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, gv), pf, z ? zero16() : adv[tt]);
+            s16x4 q1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt] + ro));
+            s16x4 q2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsQ + ca[2 * tt + 1] + ro));
+            s16x8 qv = {q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+            adk[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, qv), sf, z ? zero16() : adk[tt]);
           }
         }
       }
-      if (qt + 1 < nqt) put(bsel ^ 1, nxt);
-      __syncthreads();
     }
-  }
+    if (qt + 1 < nqt) put(bsel ^ 1, nxt);
+    __syncthreads();
+  };
+  auto sweep = [&](auto compute_c) {
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    step(0, B0{}, std::true_type{}, compute_c);
+    for (int qt = 1; qt < nqt; qt += 2) {
+      step(qt, B1{}, std::false_type{}, compute_c);
+      if (qt + 1 < nqt) step(qt + 1, B0{}, std::false_type{}, compute_c);
+    }
+  };
+  if (active) sweep(std::true_type{});   // waves past the last key only stage and sync
+  else sweep(std::false_type{});
   if (active) {
     const int k0 = kb * BK + w * 32;
     char* scr = smem + w * 32 * DP * 2;

@@ -14,9 +14,11 @@
 //   * lazy rescale (T13, threshold 2^8) decided wave-uniformly before any P of the tile is
 //     exponentiated, as in the v1 kernel.
 // One wave owns 32 query rows (query on the MFMA lane, "swapped" S^T = K Q^T), NW waves share
-// each 64-key K/V tile staged global -> registers -> LDS (issued two tiles ahead, written one
-// tile ahead; one barrier per tile).
+// each 64-key K/V tile staged global -> registers -> LDS (issue early, write late; one barrier
+// per tile).
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace sae {
@@ -68,7 +70,7 @@ struct F2Stage {
   }
 };
 
-template <int DP, int NW, bool LSUM>
+template <int DP, int NW, bool LSUM, bool FIRST>
 __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
                                           f32x16& lacc, float& m, float& l, int nvalid, float sl2,
                                           const unsigned* ka, const unsigned* va, int h) {
@@ -105,7 +107,9 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
   }
   mx = xhalf_max(mx) * sl2;
-  if (!__all(mx - m <= 8.f)) {
+  if constexpr (FIRST) {   // first tile: nothing accumulated yet, the running max starts here
+    m = mx;
+  } else if (!__all(mx - m <= 8.f)) {
     const float mn = fmaxf(m, mx);
     const float alpha = ex2(m - mn);
     m = mn;
@@ -134,7 +138,7 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 #pragma unroll
       for (int r = 0; r < 16; ++r) ls += s1[r];
     }
-    l += ls;
+    l = FIRST ? ls : l + ls;
   }
   bf16x8 ones;
 #pragma unroll
@@ -150,9 +154,10 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
       s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
       typedef __attribute__((ext_vector_type(8))) short s16x8;
       s16x8 vv = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
-      acco[t] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), pf, acco[t]);
+      // first tile, first 16 keys: the accumulators start from the MFMA's zero C operand
+      acco[t] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), pf, (FIRST && s2 == 0) ? zero16() : acco[t]);
     }
-    if constexpr (LSUM) lacc = MF<__bf16>::mma(ones, pf, lacc);
+    if constexpr (LSUM) lacc = MF<__bf16>::mma(ones, pf, (FIRST && s2 == 0) ? zero16() : lacc);
   }
   if (two) {
 #pragma unroll
@@ -196,24 +201,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
 
   wg_stamp(a.dbgbuf, a.dbg, 0);
   if (a.dbg & 4) return;
-  // K/V tiles: two register stages in flight (tile t + 2 is loaded while tile t computes and
-  // tile t + 1, loaded one tile earlier, is written to LDS at its end)
-  F2Stage<DP, NW> kst[2], vst[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    kst[r].init(tid, a.ks[1], a.D);
-    vst[r].init(tid, a.vs[1], a.D);
-  }
+  // K/V tiles staged global -> registers -> LDS: tile t + 1 is loaded while tile t computes
+  // (a second register stage in flight measured no faster and costs the third wave per SIMD)
+  F2Stage<DP, NW> kst, vst;
+  kst.init(tid, a.ks[1], a.D);
+  vst.init(tid, a.vs[1], a.D);
   const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
   const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
   const unsigned kstep = (unsigned)(64 * a.ks[1] * 2), vstep = (unsigned)(64 * a.vs[1] * 2);
   const int nkt = (a.Nk + 63) / 64;
-  kst[0].load(rk, 0);
-  vst[0].load(rv, 0);
-  if (nkt > 1) {
-    kst[1].load(rk, kstep);
-    vst[1].load(rv, vstep);
-  }
+  kst.load(rk, 0);
+  vst.load(rv, 0);
 
   // query fragments (row q, head-dim 16s + 8h .. +7), zero past Nq / D
   bf16x8 qf[NS];
@@ -242,39 +240,47 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
     }
   }
 
-  f32x16 acco[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acco[t] = zero16();
-  f32x16 lacc = zero16();
+  f32x16 acco[NT], lacc;   // written first by the peeled first tile (zero C operand)
   float m = -kInf, l = 0.f;
   const float sl2 = a.scale * kLog2e;
 
-  kst[0].write(smem);
-  vst[0].write(smem + TILE);
+  kst.write(smem);
+  vst.write(smem + TILE);
   vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   wg_stamp(a.dbgbuf, a.dbg, 1);
-  // two tiles per trip: buffer 0 then buffer 1 (immediate LDS offsets)
-  for (int kt = 0; kt < nkt; kt += 2) {
-#pragma unroll
-    for (int bsel = 0; bsel < 2; ++bsel) {
-      const int t = kt + bsel;
-      if (t >= nkt) break;
-      char* cur = smem + bsel * 2 * TILE;
-      char* nxt = smem + (bsel ^ 1) * 2 * TILE;
-      if (t + 2 < nkt && !(a.dbg & 1)) {   // register set bsel went to LDS at the end of tile t - 1
-        kst[bsel].load(rk, (unsigned)(t + 2) * kstep);
-        vst[bsel].load(rv, (unsigned)(t + 2) * vstep);
-      }
-      if (active && !(a.dbg & 2))
-        fwd2_tile<DP, NW, LSUM>(cur, cur + TILE, qf, acco, lacc, m, l, min(64, a.Nk - 64 * t), sl2, ka, va, h);
-      if (t + 1 < nkt) {
-        kst[bsel ^ 1].write(nxt);
-        vst[bsel ^ 1].write(nxt + TILE);
-      }
-      __syncthreads();
+  // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1 into the other
+  // buffer, barrier.  Buffer selection and the peeled first tile are compile-time, so the
+  // first tile's zero accumulators become the MFMA's C operand and its rescale disappears.
+  auto step = [&](int t, auto bsel_c, auto first_c, auto compute_c) {
+    constexpr int bsel = decltype(bsel_c)::value;
+    char* cur = smem + bsel * 2 * TILE;
+    char* nxt = smem + (bsel ^ 1) * 2 * TILE;
+    if (t + 1 < nkt) {
+      kst.load(rk, (unsigned)(t + 1) * kstep);
+      vst.load(rv, (unsigned)(t + 1) * vstep);
     }
-  }
+    if constexpr (decltype(compute_c)::value)
+      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value>(cur, cur + TILE, qf, acco, lacc, m, l,
+                                                        min(64, a.Nk - 64 * t), sl2, ka, va, h);
+    if (t + 1 < nkt) {
+      kst.write(nxt);
+      vst.write(nxt + TILE);
+    }
+    __syncthreads();
+  };
+  auto sweep = [&](auto compute_c) {
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    step(0, B0{}, std::true_type{}, compute_c);
+    for (int t = 1; t < nkt; t += 2) {
+      step(t, B1{}, std::false_type{}, compute_c);
+      if (t + 1 < nkt) step(t + 1, B0{}, std::false_type{}, compute_c);
+    }
+  };
+  // waves past the last query row only stage tiles and meet the barriers
+  if (active) sweep(std::true_type{});
+  else sweep(std::false_type{});
 
   wg_stamp(a.dbgbuf, a.dbg, 2);
   if (!active || (a.dbg & 8)) return;

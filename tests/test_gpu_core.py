@@ -184,3 +184,24 @@ def test_fwd_variants(dev, monkeypatch, var, B, Nq, Nk, H, D):
     mx = s.max(-1, keepdims=True)
     lse_ref = (mx + np.log(np.exp(s - mx).sum(-1, keepdims=True)))[..., 0]
     assert np.abs(lse.float().cpu().numpy() - lse_ref).max() <= 1e-3 * max(1.0, np.abs(lse_ref).max())
+
+
+@pytest.mark.parametrize("var", [3, 4, 5])
+@pytest.mark.parametrize("B,Nq,Nk,H,D", VARIANT_CASES)
+def test_bwd_variants(dev, monkeypatch, var, B, Nq, Nk, H, D):
+    """Every bf16 backward schedule selectable by SAE_BWD_VARIANT matches the oracle gradients."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    monkeypatch.setenv("SAE_BWD_VARIANT", str(var))
+    rng = np.random.default_rng(10 + var)
+    q, k, v = (randn(rng, (B, n, H, D), "bf16") for n in (Nq, Nk, Nk))
+    do = randn(np.random.default_rng(2), (B, Nq, H, D), "bf16")
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=torch.bfloat16, requires_grad=True) for x in (q, k, v))
+    o = ops.attention(tq, tk, tv)
+    o.backward(torch.tensor(do, device=dev, dtype=torch.bfloat16))
+    torch.cuda.synchronize()
+    g = R.attention_core_bwd(q, k, v, do)
+    for name, t in (("dq", tq), ("dk", tk), ("dv", tv)):
+        err = rel_err(t.grad, g[name])
+        assert err <= TOL["bf16"], f"{name}: rel err {err:.3e}"
