@@ -7,13 +7,17 @@ at N=1, configs[2]-style DP scaling at N>1) with the fused HIP attention on the 
 
 One process per GPU; the batch (128 images per GPU, synthetic N(0,1) images + uniform labels,
 resident in HBM) is sharded across ranks, gradients are all-reduced over RCCL (DDP buckets
-overlapped with the backward).  W untimed warm-up steps, then exactly K steps bracketed by a
-barrier + device synchronisation on both sides; the max elapsed time over ranks is used.
+overlapped with the backward); at N=1 the whole step (forward, loss, backward, AdamW) is one HIP
+graph, replayed (--eager: launch it op by op).  W untimed warm-up steps, then exactly K steps
+bracketed by a barrier + device synchronisation on both sides; the max elapsed time over ranks is
+used.
 Rank 0 prints ONE JSON line:
   value        = whole-job training images/s (all ranks)
   roofline     = the fused attention op of this workload (fwd + bwd = 3 launches: attn_fwd,
                  attn_bwd_dq (+ delta), attn_bwd_dkdv), timed live with HIP events on its launch
-                 stream inside the timed region; algorithmic FLOPs/bytes per call (DESIGN.md §4);
+                 stream inside the timed region (graph mode: over 3 eager steps right after it,
+                 since graph replays carry no host events); algorithmic FLOPs/bytes per call
+                 (DESIGN.md §4);
                  traffic = HBM bytes per call from profiles/pmc_traffic.json (rocprofv3 PMC)
   cpu_baseline = the numpy port (oracle/vit_ref.py) of the same training step on a bounded
                  sample, on this host's cores (rank 0, N=1 only)
@@ -166,6 +170,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-headline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="training loop only (for rocprofv3 runs)")
+    ap.add_argument("--eager", action="store_true", help="N=1: eager step instead of the HIP-graph replay")
     args = ap.parse_args()
 
     import torch
@@ -182,7 +187,10 @@ def main():
     torch.manual_seed(0)
     model = vit.create_model(args.model, 1000, torch.bfloat16, device=dev)
     B = args.batch
-    step = train.TrainStep(model, global_batch=B * world, device=dev)
+    # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1: the
+    # eager DDP step (RCCL all-reduce overlapped with the backward through DDP's bucket hooks)
+    use_graph = world == 1 and not args.eager
+    step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, 224, 224, 3, device=dev, generator=g)
     labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
@@ -191,7 +199,8 @@ def main():
         step(images, labels)
     torch.cuda.synchronize()
     timer = ops.KernelTimer()
-    ops.set_kernel_timer(timer)
+    if not use_graph:   # eager launches: the attention events sit inside the timed region
+        ops.set_kernel_timer(timer)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -203,6 +212,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ops.set_kernel_timer(None)
+    if use_graph:
+        # graph replays carry no host-side events: time the same kernels with HIP events on their
+        # launch stream over eager steps of the same workload, right after the timed region
+        ops.set_kernel_timer(timer)
+        for _ in range(3):
+            step._eager(images, labels)
+        ops.set_kernel_timer(None)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -229,7 +245,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
         "config": {"workload": f"DeiT-S/16 224px bf16 data-parallel training step (fused attention fwd+bwd)",
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
-                   "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}"},
+                   "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
+                   "step": "hip_graph_replay" if use_graph else "eager"},
         "roofline": roof,
         "attention": {"calls_per_step": ksum["attn_fwd"]["launches"] // args.steps, "fwd_ms": round(fwd_ms, 4),
                       "bwd_ms": round(bwd_ms, 4), "tflops": roof["tflops"],

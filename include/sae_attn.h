@@ -154,6 +154,26 @@ int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, in
                 const void* dy, int64_t ldy, float* dw, int64_t ldw, float* db,
                 int32_t accumulate, void* workspace);
 
+/* Forward and input-gradient GEMMs of the projections and the FF block (the dot_generals of
+   Flax Dense / DenseGeneral, attention.py:29-37,60-63 and ff.py:8-34), with the FF block's
+   nn.gelu (tanh form, ff.py:27) and its derivative fused into the epilogue:
+     acc[m][n] = sum_k a[m][k] * bt[n][k]      a bf16 [M][K] (lda), bt bf16 [N][K] (ldb)
+     SAE_EPI_NONE : c = bf16(acc + bias)
+     SAE_EPI_GELU : c2 = h = bf16(acc + bias), c = bf16(gelu(h))
+     SAE_EPI_DGELU: c = bf16(bf16(acc) * gelu'(aux))   (aux bf16 [M][N], ldaux; bias NULL)
+   c, c2 bf16 [M][N] (ldc); bias fp32 [N] or NULL.  K a multiple of 64; N, lda, ldb, ldc
+   multiples of 8; pointers 16-byte aligned.  A Dense forward passes the transposed bf16
+   kernel as bt (see sae_weight_cast); its input gradient passes the kernel itself. */
+#define SAE_EPI_NONE 0
+#define SAE_EPI_GELU 1
+#define SAE_EPI_DGELU 2
+int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
+                const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
+                int32_t epilogue, const void* aux, int64_t ldaux, void* c2);
+/* fp32 Dense kernel w [K][N] -> bf16 w16 [K][N] and/or its transpose wt16 [N][K] (either may
+   be NULL): the compute-dtype casts of Flax Dense (kernel cast to dtype). */
+int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w16, void* wt16);
+
 /* Residual add + LayerNorm of the encoder blocks around the path (models/vit.py:19-31,57;
    Flax nn.LayerNorm: fp32 statistics, eps, output in the compute dtype):
      xout = x + delta (fp32; when delta != NULL), y = LN(xout) * gamma + beta in bf16,

@@ -18,6 +18,7 @@
 #include "fwd3.h"
 #include "bwd2.h"
 #include "gemm_dw.h"
+#include "gemm_nt.h"
 #include "ln.h"
 
 using namespace sae;
@@ -697,6 +698,70 @@ int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, in
   const unsigned rb = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
   hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3(rb, db ? 2 : 1), dim3(256), 0, st, a);
   return check_launch("gemm_dw_reduce");
+}
+
+// ------------------------------------------------------------ forward / input-gradient GEMMs
+int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
+                int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
+                int64_t ldaux, void* c2) {
+  if (M < 1 || N < 1 || K < 1) return fail(SAE_EINVAL, "gemm_nt: M/N/K must be >= 1 (got %d/%d/%d)", M, N, K);
+  if (K % kNtK || N % 8)
+    return fail(SAE_EUNSUPPORTED, "gemm_nt: K (%d) must be a multiple of %d and N (%d) of 8", K, kNtK, N);
+  if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8)
+    return fail(SAE_EINVAL, "gemm_nt: bad leading dimensions lda %lld ldb %lld ldc %lld", (long long)lda,
+                (long long)ldb, (long long)ldc);
+  if (!a || !bt || !c) return fail(SAE_EINVAL, "gemm_nt: a/bt/c must be non-NULL");
+  if (epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_DGELU)
+    return fail(SAE_EINVAL, "gemm_nt: unknown epilogue %d", epilogue);
+  if (epilogue == SAE_EPI_GELU && !c2) return fail(SAE_EINVAL, "gemm_nt: the GELU epilogue needs c2 (pre-activation out)");
+  if (epilogue == SAE_EPI_DGELU && (!aux || ldaux < N || ldaux % 8 || bias))
+    return fail(SAE_EINVAL, "gemm_nt: the GELU-derivative epilogue needs aux (ldaux >= N, multiple of 8) and no bias");
+  if (!aligned16(a) || !aligned16(bt) || !aligned16(c) || !aligned16(c2) || !aligned16(aux) || !aligned16(bias))
+    return fail(SAE_EINVAL, "gemm_nt: a, bt, c, c2, aux and bias must be 16-byte aligned");
+  if ((long long)kNtT * std::max(lda, ldb) * 2 >= (1LL << 31))
+    return fail(SAE_EUNSUPPORTED, "gemm_nt: a 128-row block exceeds 32-bit buffer addressing");
+  NtArgs g;
+  memset(&g, 0, sizeof g);
+  g.a = reinterpret_cast<const __bf16*>(a);
+  g.bt = reinterpret_cast<const __bf16*>(bt);
+  g.bias = bias;
+  g.aux = reinterpret_cast<const __bf16*>(aux);
+  g.c = reinterpret_cast<__bf16*>(c);
+  g.c2 = reinterpret_cast<__bf16*>(c2);
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.ldaux = ldaux;
+  hipStream_t st = (hipStream_t)stream;
+  const long long grid = (long long)((M + kNtT - 1) / kNtT) * ((N + kNtT - 1) / kNtT);
+  if (grid >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "gemm_nt: grid too large");
+  const size_t lds = 4 * kNtT * kNtK * 2;
+  switch (epilogue) {
+    case SAE_EPI_NONE:
+      if (int rc = lds_attr((const void*)gemm_nt_kernel<kEpiNone>, lds)) return rc;
+      hipLaunchKernelGGL(gemm_nt_kernel<kEpiNone>, dim3((unsigned)grid), dim3(256), lds, st, g);
+      break;
+    case SAE_EPI_GELU:
+      if (int rc = lds_attr((const void*)gemm_nt_kernel<kEpiGelu>, lds)) return rc;
+      hipLaunchKernelGGL(gemm_nt_kernel<kEpiGelu>, dim3((unsigned)grid), dim3(256), lds, st, g);
+      break;
+    default:
+      if (int rc = lds_attr((const void*)gemm_nt_kernel<kEpiDGelu>, lds)) return rc;
+      hipLaunchKernelGGL(gemm_nt_kernel<kEpiDGelu>, dim3((unsigned)grid), dim3(256), lds, st, g);
+      break;
+  }
+  return check_launch("gemm_nt");
+}
+
+int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w16, void* wt16) {
+  if (K < 1 || N < 1) return fail(SAE_EINVAL, "weight_cast: K/N must be >= 1 (got %d/%d)", K, N);
+  if (!w || (!w16 && !wt16)) return fail(SAE_EINVAL, "weight_cast: w and at least one output must be non-NULL");
+  hipLaunchKernelGGL(weight_cast_kernel, dim3((N + 31) / 32, (K + 31) / 32), dim3(256), 0, (hipStream_t)stream, w,
+                     reinterpret_cast<__bf16*>(w16), reinterpret_cast<__bf16*>(wt16), K, N);
+  return check_launch("weight_cast");
 }
 
 // ------------------------------------------------------------ residual add + LayerNorm

@@ -1,0 +1,241 @@
+// gemm_nt.h -- forward / input-gradient GEMMs of the projections and the FF block, with the
+// FF block's tanh-GELU and its derivative fused into the epilogue.
+//
+//   c[m][n] = epi( sum_k a[m][k] * bt[n][k] (+ bias[n]) )
+//
+// a [M][K] bf16 (tokens, row stride lda), bt [N][K] bf16 (output features, row stride ldb): both
+// operands are K-contiguous ("NT").  The forward of a Flax Dense (kernel [in, out]) passes the
+// transposed bf16 kernel copy; its input gradient dX = dY W^T passes the kernel as it is.
+// Epilogues (ff.py:8-34: Dense -> nn.gelu (tanh form) -> Dense):
+//   kEpiNone : c = bf16(acc + bias)
+//   kEpiGelu : c2 = h = bf16(acc + bias) (saved for the backward), c = bf16(gelu(h))
+//   kEpiDGelu: c = bf16(bf16(acc) * gelu'(aux))   (aux = the saved h; the FF block's dH)
+// which removes the two elementwise HBM passes (GELU forward, GELU backward) per FF block.
+//
+// Structure (gfx950): a 128 x 128 output tile per 256-thread workgroup, 4 waves of 64 x 64 (2 x 2
+// v_mfma_f32_32x32x16_bf16 accumulators); 64-deep K stages staged global -> registers -> LDS
+// ([128 rows][64 k] images, 128-byte rows XOR-swizzled per row: conflict-free ds_read_b128), two
+// LDS buffers, loads issued two stages ahead.  The MFMA runs with the output feature as the
+// accumulator row and the token on the lane, so the epilogue writes each token's features as
+// packed bf16x4 into a per-wave LDS image and stores whole 128-byte row segments.
+// XCD-aware order: the N tiles of one token block are consecutive on one XCD (the token rows are
+// fetched from HBM once per XCD; the small weight stays L2-resident).
+#pragma once
+#include "common.h"
+
+namespace sae {
+
+enum { kEpiNone = 0, kEpiGelu = 1, kEpiDGelu = 2 };
+
+struct NtArgs {
+  const __bf16* a;     // [M][K], row stride lda
+  const __bf16* bt;    // [N][K], row stride ldb
+  const float* bias;   // [N] or null
+  const __bf16* aux;   // [M][N] row stride ldaux (kEpiDGelu)
+  __bf16* c;           // [M][N] row stride ldc
+  __bf16* c2;          // [M][N] row stride ldc (kEpiGelu: pre-activation)
+  int M, N, K;
+  long long lda, ldb, ldc, ldaux;
+};
+
+constexpr int kNtT = 128;   // output tile edge
+constexpr int kNtK = 64;    // K per stage
+
+// tanh-GELU (Flax nn.gelu default; torch approximate="tanh"): 0.5 x (1 + tanh(y)),
+// y = sqrt(2/pi) (x + 0.044715 x^3) = x * sigmoid(2y)
+constexpr float kGeluB = 0.7978845608028654f;
+constexpr float kGeluK = 0.044715f;
+
+__device__ __forceinline__ float gelu_sig(float x) {   // sigmoid(2y)
+  const float y2 = x * (kGeluB + (kGeluB * kGeluK) * x * x);
+  return __builtin_amdgcn_rcpf(1.f + ex2(-2.f * kLog2e * y2));
+}
+__device__ __forceinline__ float gelu_f(float x) { return x * gelu_sig(x); }
+__device__ __forceinline__ float dgelu_f(float x) {
+  const float s = gelu_sig(x);
+  return s + 2.f * x * s * (1.f - s) * (kGeluB + (3.f * kGeluB * kGeluK) * x * x);
+}
+
+// one operand's 128 x 64 stage: 1024 16-byte chunks, 4 per thread
+struct NtStage {
+  uint4 v[4];
+  unsigned goff[4];
+  unsigned loff[4];
+  __device__ __forceinline__ void init(int tid, long long ld) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      const int r = id >> 3, c = id & 7;
+      goff[i] = (unsigned)(((long long)r * ld + 8 * c) * 2);
+      loff[i] = r * 128 + 16 * (c ^ swz<64>(r));
+    }
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned koff) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i] + koff, 0, 0));
+  }
+  __device__ __forceinline__ void write(char* img) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
+  }
+};
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = kNtT * kNtK * 2;   // 16 KiB per operand image
+  const int tn = (a.N + kNtT - 1) / kNtT;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tn, nt = bid % tn;
+  const int m0 = mt * kNtT, n0 = nt * kNtT;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;   // this wave's 64 (tokens) x 64 (features) quarter
+
+  // rows past M / N read zero through the descriptors' range checks
+  const __amdgpu_buffer_rsrc_t ra = row_rsrc(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
+  const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
+  NtStage as[2], bs[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    as[q].init(tid, a.lda);
+    bs[q].init(tid, a.ldb);
+  }
+  const int nst = a.K / kNtK;
+  as[0].load(ra, 0);
+  bs[0].load(rb, 0);
+  if (nst > 1) {
+    as[1].load(ra, kNtK * 2);
+    bs[1].load(rb, kNtK * 2);
+  }
+  f32x16 acc[2][2];   // [feature sub-tile t][token sub-tile u]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[t][u] = zero16();
+
+  as[0].write(smem);
+  bs[0].write(smem + IMG);
+  __syncthreads();
+  for (int st0 = 0; st0 < nst; st0 += 2) {
+#pragma unroll
+    for (int bsel = 0; bsel < 2; ++bsel) {
+      const int st = st0 + bsel;
+      if (st >= nst) break;
+      const char* ima = smem + bsel * 2 * IMG;
+      const char* imb = ima + IMG;
+      char* nxt = smem + (bsel ^ 1) * 2 * IMG;
+      if (st + 2 < nst) {   // register set bsel went to LDS at the end of stage st - 1
+        as[bsel].load(ra, (unsigned)(st + 2) * (kNtK * 2));
+        bs[bsel].load(rb, (unsigned)(st + 2) * (kNtK * 2));
+      }
+#pragma unroll
+      for (int s = 0; s < kNtK / 16; ++s) {
+        const bf16x8 b0 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + r, s, h);
+        const bf16x8 b1 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + 32 + r, s, h);
+        const bf16x8 a0 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + r, s, h);
+        const bf16x8 a1 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + 32 + r, s, h);
+        acc[0][0] = MF<__bf16>::mma(b0, a0, acc[0][0]);
+        acc[0][1] = MF<__bf16>::mma(b0, a1, acc[0][1]);
+        acc[1][0] = MF<__bf16>::mma(b1, a0, acc[1][0]);
+        acc[1][1] = MF<__bf16>::mma(b1, a1, acc[1][1]);
+      }
+      if (st + 1 < nst) {
+        as[bsel ^ 1].write(nxt);
+        bs[bsel ^ 1].write(nxt + IMG);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: accumulator row = feature nb + 32t + row_of(reg, h), column = token (lane)
+  const int nb = n0 + 64 * wn;
+  if (EPI != kEpiDGelu && a.bias) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = nb + 32 * t + 8 * g + 4 * h;
+        const f32x4 bv = (n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[t][0][4 * g + e] += bv[e];
+          acc[t][1][4 * g + e] += bv[e];
+        }
+      }
+  }
+  char* scratch = smem + w * (32 * 64 * 2);   // 4 KiB per wave; the stage buffers are free now
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
+  const int c8 = lane & 7;          // 16-byte chunk of the row segment (features nb + 8 c8 ..)
+  const int n = nb + 8 * c8;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x4 v = {(__bf16)acc[t][u][4 * g], (__bf16)acc[t][u][4 * g + 1], (__bf16)acc[t][u][4 * g + 2],
+                          (__bf16)acc[t][u][4 * g + 3]};
+        *reinterpret_cast<bf16x4*>(scratch + r * 128 + 16 * ((4 * t + g) ^ swz<64>(r)) + 8 * h) = v;
+      }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int rr = 8 * it + (lane >> 3);
+      const int m = m0 + 64 * wm + 32 * u + rr;
+      const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * 128 + 16 * (c8 ^ swz<64>(rr)));
+      if (m < a.M && n < a.N) {
+        if constexpr (EPI == kEpiNone) {
+          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
+        } else if constexpr (EPI == kEpiGelu) {
+          *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
+          const bf16x8v hv = __builtin_bit_cast(bf16x8v, raw);
+          bf16x8v y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = (__bf16)gelu_f((float)hv[e]);
+          *reinterpret_cast<bf16x8v*>(a.c + (long long)m * a.ldc + n) = y;
+        } else {
+          const bf16x8v dv = __builtin_bit_cast(bf16x8v, raw);
+          const bf16x8v hv = *reinterpret_cast<const bf16x8v*>(a.aux + (long long)m * a.ldaux + n);
+          bf16x8v y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = (__bf16)((float)dv[e] * dgelu_f((float)hv[e]));
+          *reinterpret_cast<bf16x8v*>(a.c + (long long)m * a.ldc + n) = y;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// fp32 Dense kernel w [K][N] -> bf16 copies: w16 [K][N] (may be null) and its transpose
+// wt16 [N][K] (may be null).  32 x 32 tiles through LDS, 4 elements per thread (many small
+// workgroups: the weights are < 10 MB, so this is latency-, not bandwidth-bound).
+__global__ __launch_bounds__(256) void weight_cast_kernel(const float* w, __bf16* w16, __bf16* wt16, int K, int N) {
+  __shared__ float tile[32][33];
+  const int k0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + ty + 8 * i, n = n0 + tx;
+    v[i] = (k < K && n < N) ? w[(long long)k * N + n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + ty + 8 * i, n = n0 + tx;
+    if (w16 && k < K && n < N) w16[(long long)k * N + n] = (__bf16)v[i];
+    tile[ty + 8 * i][tx] = v[i];
+  }
+  if (!wt16) return;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + ty + 8 * i, k = k0 + tx;
+    if (k < K && n < N) wt16[(long long)n * K + k] = (__bf16)tile[tx][ty + 8 * i];
+  }
+}
+
+}  // namespace sae

@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "dense", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -386,10 +386,14 @@ class _Dense(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, dt):
         I, J = w.shape
-        wd = w.to(dt)
         x2 = x.to(dt).reshape(-1, I)
-        # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
-        y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
+        if dt == torch.bfloat16 and w.dtype == torch.float32 and use_gemm_nt(I) and _nt_ok(x2, J):
+            wd, wt = weight_cast(w)                       # both layouts in one pass
+            y = gemm_nt(x2, wt, b)                        # bias in the epilogue
+        else:
+            wd = w.to(dt)
+            # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
+            y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
         ctx.save_for_backward(x2, wd)
         ctx.has_b, ctx.xshape, ctx.wdtype, ctx.xdtype = b is not None, x.shape, w.dtype, x.dtype
         return y.view(*x.shape[:-1], J)
@@ -401,7 +405,10 @@ class _Dense(torch.autograd.Function):
         dy2 = dy.reshape(-1, J)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
             dy2 = dy2.contiguous()
-        dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
+        if use_gemm_nt(J) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
+            dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
+        else:
+            dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
         if _dw_ok(x2, dy2):
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
@@ -416,6 +423,122 @@ class _Dense(torch.autograd.Function):
 def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
     """Projection of the hot path: ``x @ w (+ b)`` in ``dtype`` with fp32 parameter gradients."""
     return _Dense.apply(x, w, b, dtype)
+
+
+# ------------------------------------------------- forward / input-gradient GEMMs (sae_gemm_nt)
+EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
+
+
+# sae_gemm_nt vs the library GEMM at the training shapes (tools/gemm_probe.py,
+# profiles/r01_gemm_probe_v11.txt): the HIP kernel wins for reduction depths <= 384 (DeiT-S QKV
+# forward 37 vs 78 us, output projection 17 vs 21 us), the library for the deeper ones
+# (K = 768 .. 1536); the FF block always fuses its GELU / GELU' into sae_gemm_nt.
+GEMM_NT_MAX_K = 512
+
+
+def use_gemm_nt(K: int) -> bool:
+    return K <= GEMM_NT_MAX_K
+
+
+def _nt_ok(a2: torch.Tensor, N: int) -> bool:
+    K = a2.shape[1]
+    return (a2.is_cuda and a2.dtype == torch.bfloat16 and K % 64 == 0 and N % 8 == 0 and a2.stride(1) == 1
+            and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0)
+
+
+def weight_cast(w: torch.Tensor, plain: bool = True, transposed: bool = True):
+    """fp32 Dense kernel [K, N] -> (bf16 [K, N] or None, bf16 [N, K] or None) in one HIP pass."""
+    lib = L.load()
+    _require_gpu(w)
+    K, N = w.shape
+    w = w.contiguous()
+    w16 = torch.empty((K, N), dtype=torch.bfloat16, device=w.device) if plain else None
+    wt16 = torch.empty((N, K), dtype=torch.bfloat16, device=w.device) if transposed else None
+    L.check(lib.sae_weight_cast(_stream(w), K, N, _ptr(w), _ptr(w16), _ptr(wt16)))
+    return w16, wt16
+
+
+def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
+            aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """``epi(a2 @ bt^T (+ bias))`` through ``sae_gemm_nt``: a2 [M, K], bt [N, K] bf16.  Returns c,
+    or (c, h) for the GELU epilogue (c = gelu(h), h = the bf16 pre-activation)."""
+    lib = L.load()
+    _require_gpu(a2, bt)
+    M, K = a2.shape
+    N = bt.shape[0]
+    if bt.shape[1] != K:
+        raise ValueError(f"gemm_nt: a2 {tuple(a2.shape)} and bt {tuple(bt.shape)} disagree on K")
+    if bt.stride(1) != 1:
+        bt = bt.contiguous()
+    c = out if out is not None else torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
+    c2 = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device) if epilogue == EPI_GELU else None
+    if aux is not None and aux.stride(1) != 1:
+        aux = aux.contiguous()
+    if bias is not None:
+        bias = bias.float().contiguous()
+    L.check(lib.sae_gemm_nt(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias), _ptr(c),
+                            c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0, _ptr(c2)))
+    return (c, c2) if epilogue == EPI_GELU else c
+
+
+class _FFBlock(torch.autograd.Function):
+    """ff.py:8-34 in bf16: ``Dense_1(gelu(Dense_0(x)))`` with the GELU fused into Dense_0's GEMM
+    epilogue (saving the pre-activation h) and its derivative fused into the epilogue of Dense_1's
+    input-gradient GEMM; weight / bias gradients through ``sae_gemm_dw``."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1):
+        I, Hd = w0.shape
+        x2 = x.to(torch.bfloat16).reshape(-1, I)
+        if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        w0p, w0t = weight_cast(w0)
+        w1p, _ = weight_cast(w1, transposed=False)
+        a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
+        if use_gemm_nt(Hd):
+            y = gemm_nt(a, w1p.t().contiguous(), b1)
+        else:   # deep reduction (K = hidden): the library GEMM is faster there
+            y = torch.addmm(b1.to(torch.bfloat16), a, w1p) if b1 is not None else a @ w1p
+        ctx.save_for_backward(x2, h, a, w0p, w1p)
+        ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
+        return y.view(*x.shape[:-1], w1.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, a, w0p, w1p = ctx.saved_tensors
+        I, Hd = w0p.shape
+        O = w1p.shape[1]
+        dy2 = dy.to(torch.bfloat16).reshape(-1, O)
+        if dy2.stride(1) != 1 or dy2.stride(0) % 8 or dy2.data_ptr() % 16:
+            dy2 = dy2.contiguous()
+        dh = gemm_nt(dy2, w1p, None, EPI_DGELU, aux=h)            # dA W1^T, times gelu'(h)
+        dw1 = torch.empty((Hd, O), dtype=torch.float32, device=dy2.device)
+        db1 = torch.empty((O,), dtype=torch.float32, device=dy2.device) if ctx.has_b[1] else None
+        gemm_dw(a, dy2, dw1, db1)
+        dx = gemm_nt(dh, w0p) if use_gemm_nt(Hd) else dh @ w0p.t()   # dH W0^T
+        dw0 = torch.empty((I, Hd), dtype=torch.float32, device=dy2.device)
+        db0 = torch.empty((Hd,), dtype=torch.float32, device=dy2.device) if ctx.has_b[0] else None
+        gemm_dw(x2, dh, dw0, db0)
+        return dx.view(ctx.xshape).to(ctx.xdtype), dw0, db0, dw1, db1
+
+
+FF_FUSED = True   # tools/ab_step.py flips this to A/B against the library GEMM + torch GELU path
+
+
+def ff_block_ok(x: torch.Tensor, w0: torch.Tensor, w1: torch.Tensor) -> bool:
+    if not FF_FUSED:
+        return False
+    I, Hd = w0.shape
+    O = w1.shape[1]
+    return (x.is_cuda and w0.dtype == w1.dtype == torch.float32 and I % 64 == 0 and Hd % 64 == 0 and O % 8 == 0
+            and w1.shape[0] == Hd)
+
+
+def ff_block(x: torch.Tensor, w0: torch.Tensor, b0: Optional[torch.Tensor], w1: torch.Tensor,
+             b1: Optional[torch.Tensor]) -> torch.Tensor:
+    """Flax FFBlock (ff.py:8-34, dropout 0) in bf16 with fp32 params: x [.., I] -> [.., O]."""
+    _require_gpu(x, w0, w1)
+    return _FFBlock.apply(x, w0, b0, w1, b1)
 
 
 # ------------------------------------------------------------------ residual add + LayerNorm

@@ -48,8 +48,15 @@ class TrainStep:
     all-reduce overlapped with it when world > 1) + optimizer update.  No host sync."""
 
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
-                 label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None):
+                 label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
+                 graph: bool = False):
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        # One HIP graph for the whole step (forward, loss, backward, AdamW): the eager step spends
+        # ~10 ms/step of host time submitting ~600 launches (tools/ab_step.py), as long as the GPU
+        # needs to run them.  Single-process only: with world > 1 the DDP step stays eager so the
+        # RCCL all-reduce keeps overlapping the backward through DDP's bucket hooks.
+        self.graph = bool(graph) and self.world == 1 and torch.cuda.is_available()
+        self._g = None
         self.model = model
         if self.world > 1:
             self.ddp = torch.nn.parallel.DistributedDataParallel(
@@ -60,16 +67,45 @@ class TrainStep:
         base_lr = lr * (global_batch / 512)
         params = [p for p in model.parameters() if p.requires_grad]
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
+        if self.graph:
+            kw["capturable"] = True   # step counters on the device: replayable
         try:
             self.opt = torch.optim.AdamW(params, fused=True, **kw)
         except (RuntimeError, TypeError):
             self.opt = torch.optim.AdamW(params, foreach=True, **kw)
         self.smoothing = label_smoothing
 
-    def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    def _eager(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         self.opt.zero_grad(set_to_none=True)
         logits = self.ddp(images, is_training=True)
         loss = smoothed_cross_entropy(logits, labels, self.smoothing)
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+    def _capture(self, images: torch.Tensor, labels: torch.Tensor):
+        self._images = images.clone()
+        self._labels = labels.clone()
+        s = torch.cuda.Stream(device=images.device)
+        s.wait_stream(torch.cuda.current_stream(images.device))
+        with torch.cuda.stream(s):   # warm-up on a side stream (allocator / library state)
+            for _ in range(2):
+                self._eager(self._images, self._labels)
+        torch.cuda.current_stream(images.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            self._loss = self._eager(self._images, self._labels)
+        self._g = g
+
+    def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        if not self.graph:
+            return self._eager(images, labels)
+        if self._g is None:
+            self._capture(images, labels)
+        if images.data_ptr() != self._images.data_ptr():
+            self._images.copy_(images)
+        if labels.data_ptr() != self._labels.data_ptr():
+            self._labels.copy_(labels)
+        self._g.replay()
+        return self._loss

@@ -12,7 +12,8 @@ cls / pos-embed params promote it, vit.py:46,85), LayerNorm eps 1e-6, tanh-GELU 
 The attention is ``layers.SelfAttentionBlock`` (fused HIP kernels).  Around it (survey §8f
 "next"): Dense / DenseGeneral go through ``ops.dense`` (library GEMM forward and input gradient,
 HIP split-token weight/bias gradients), and with a bf16 compute dtype every residual add is fused
-with the LayerNorm that follows it (``ops.add_layer_norm``, HIP); GELU stays a library op.
+with the LayerNorm that follows it (``ops.add_layer_norm``, HIP) and the FF block runs as
+``ops.ff_block`` (HIP GEMMs with the tanh-GELU and its derivative fused into their epilogues).
 """
 from __future__ import annotations
 
@@ -66,7 +67,11 @@ class FFBlock(nn.Module):
         self.Dense_1 = Dense(hid, dim, device=device)
 
     def forward(self, x, dtype):
-        return self.Dense_1(F.gelu(self.Dense_0(x, dtype), approximate="tanh"), dtype)
+        d0, d1 = self.Dense_0, self.Dense_1
+        if dtype == torch.bfloat16 and ops.ff_block_ok(x, d0.kernel, d1.kernel):
+            # GELU fused into Dense_0's GEMM epilogue, its derivative into Dense_1's dX GEMM
+            return ops.ff_block(x, d0.kernel, d0.bias, d1.kernel, d1.bias)
+        return d1(F.gelu(d0(x, dtype), approximate="tanh"), dtype)
 
 
 class EncoderBlock(nn.Module):

@@ -1,0 +1,155 @@
+"""Forward / input-gradient GEMM kernel (sae_gemm_nt) with its fused FF-block epilogues, and the
+FF block built on it (ff.py:8-34: Dense -> nn.gelu (tanh) -> Dense).
+
+References: float64 products of the same bf16 inputs; GELU / GELU' from torch's fp32
+``gelu(approximate="tanh")`` (= Flax ``nn.gelu`` default).  Outputs are bf16, so the bar is bf16
+rounding (2e-2 of the largest magnitude, the north_star bf16 tolerance); the pre-activation h and
+the weight casts are compared bit for bit where the math is exact."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (M, K, N)
+    (25216, 384, 1536),   # DeiT-S FF Dense_0 forward / Dense_1 input gradient
+    (25216, 1536, 384),   # DeiT-S FF Dense_1 forward / Dense_0 input gradient
+    (25216, 384, 1152),   # DeiT-S QKV projection
+    (197, 768, 1000),     # ragged tokens, head-like N (not a tile multiple)
+    (1000, 64, 40),       # one K stage, N below one tile
+    (130, 128, 136),
+]
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+
+
+def _inputs(dev, M, K, N, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    bt = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev, generator=g) * 0.1
+    return a, bt, bias
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_nt_plain(dev, M, K, N, bias):
+    import sae_vision_amd.ops as ops
+    a, bt, b = _inputs(dev, M, K, N, M + K + N)
+    c = ops.gemm_nt(a, bt, b if bias else None)
+    ref = a.double() @ bt.double().t()
+    if bias:
+        ref = ref + b.double()
+    assert c.shape == (M, N) and c.dtype == torch.bfloat16
+    assert _rel(c, ref) <= 1e-2
+
+
+@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136)])
+def test_gemm_nt_gelu(dev, M, K, N):
+    import sae_vision_amd.ops as ops
+    a, bt, b = _inputs(dev, M, K, N, 11)
+    y, h = ops.gemm_nt(a, bt, b, ops.EPI_GELU)
+    ref_h = a.double() @ bt.double().t() + b.double()
+    assert _rel(h, ref_h) <= 1e-2
+    # gelu applied to the kernel's own bf16 pre-activation: only the final rounding differs
+    ref_y = F.gelu(h.float(), approximate="tanh")
+    assert _rel(y, ref_y) <= 1e-2
+    assert float((y.float() - ref_y).abs().max()) <= 2 ** -7 * float(ref_y.abs().max())
+
+
+@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136)])
+def test_gemm_nt_dgelu(dev, M, K, N):
+    import sae_vision_amd.ops as ops
+    a, bt, _ = _inputs(dev, M, K, N, 12)
+    g = torch.Generator(device=dev).manual_seed(13)
+    h = (torch.randn(M, N, device=dev, generator=g) * 2).to(torch.bfloat16)
+    dh = ops.gemm_nt(a, bt, None, ops.EPI_DGELU, aux=h)
+    da = (a.double() @ bt.double().t()).to(torch.bfloat16).float()
+    hf = h.float().requires_grad_(True)
+    F.gelu(hf, approximate="tanh").backward(da)
+    assert _rel(dh, hf.grad) <= 1e-2
+
+
+def test_gemm_nt_strided_out(dev):
+    """Row-strided a (a column slice of a wider buffer) and c written into a wider buffer."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(5)
+    M, K, N = 777, 128, 64
+    aw = torch.randn(M, K + 64, device=dev, generator=g).to(torch.bfloat16)
+    a = aw[:, 64:]
+    bt = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+    cw = torch.zeros(M, N + 16, device=dev, dtype=torch.bfloat16)
+    ops.gemm_nt(a, bt, out=cw[:, :N])
+    assert _rel(cw[:, :N], a.double() @ bt.double().t()) <= 1e-2
+    assert float(cw[:, N:].abs().max()) == 0.0
+
+
+def test_gemm_nt_rejects(dev):
+    import sae_vision_amd.ops as ops
+    from sae_vision_amd._lib import SaeError
+    a = torch.zeros(64, 96, device=dev, dtype=torch.bfloat16)      # K not a multiple of 64
+    bt = torch.zeros(64, 96, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(SaeError):
+        ops.gemm_nt(a, bt)
+    a = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    bt = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(SaeError):                                   # DGELU without aux
+        ops.gemm_nt(a, bt, None, ops.EPI_DGELU)
+
+
+def test_weight_cast_exact(dev):
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(9)
+    for K, N in ((384, 1536), (1536, 384), (100, 72), (3, 5)):
+        w = torch.randn(K, N, device=dev, generator=g)
+        w16, wt16 = ops.weight_cast(w)
+        assert torch.equal(w16, w.to(torch.bfloat16))
+        assert torch.equal(wt16, w.t().contiguous().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,C", [(2 * 197, 384), (3 * 577, 768)])
+def test_ff_block_fwd_bwd(dev, M, C):
+    """ops.ff_block against the unfused bf16 path (library GEMMs + torch GELU) and an fp32 one."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(M)
+    x = torch.randn(M, C, device=dev, generator=g)
+    w0 = torch.randn(C, 4 * C, device=dev, generator=g) / C ** 0.5
+    b0 = torch.randn(4 * C, device=dev, generator=g) * 0.1
+    w1 = torch.randn(4 * C, C, device=dev, generator=g) / (4 * C) ** 0.5
+    b1 = torch.randn(C, device=dev, generator=g) * 0.1
+    dy = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
+
+    leaves = [t.clone().requires_grad_(True) for t in (x, w0, b0, w1, b1)]
+    y = ops.ff_block(leaves[0].to(torch.bfloat16), *leaves[1:])
+    y.backward(dy)
+
+    ref = [t.clone().double().requires_grad_(True) for t in (x, w0, b0, w1, b1)]
+    xb = ref[0].to(torch.bfloat16).double()
+    hr = (xb @ ref[1].to(torch.bfloat16).double() + ref[2])
+    yr = F.gelu(hr, approximate="tanh") @ ref[3].to(torch.bfloat16).double() + ref[4]
+    yr.backward(dy.double())
+    assert _rel(y, yr) <= 2e-2
+    for got, want, name in zip(leaves, ref, ("x", "w0", "b0", "w1", "b1")):
+        assert _rel(got.grad, want.grad) <= 2e-2, name
+
+
+def test_ff_block_deterministic(dev):
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(1)
+    M, C = 4 * 197, 384
+    x = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
+    w0 = torch.randn(C, 4 * C, device=dev, generator=g) / C ** 0.5
+    w1 = torch.randn(4 * C, C, device=dev, generator=g) / (4 * C) ** 0.5
+    b0, b1 = torch.zeros(4 * C, device=dev), torch.zeros(C, device=dev)
+    dy = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        ps = [t.clone().requires_grad_(True) for t in (w0, b0, w1, b1)]
+        xx = x.clone().requires_grad_(True)
+        y = ops.ff_block(xx, *ps)
+        y.backward(dy)
+        outs.append([y.detach(), xx.grad] + [p.grad for p in ps])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

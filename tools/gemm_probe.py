@@ -45,7 +45,23 @@ def main():
         ms_x = bench(lambda: dy @ b.t())
         ms_w = bench(lambda: a.t() @ dy)
         ms_h = bench(lambda: ops.gemm_dw(a, dy, dw, db))
+        bt = b.t().contiguous()
+        ms_nt = bench(lambda: ops.gemm_nt(a, bt))
+        ms_ntx = bench(lambda: ops.gemm_nt(dy, b))
         f = 2.0 * m * n * k
+        print(f"{name:9s} sae_gemm_nt fwd {ms_nt*1e3:7.1f} us {f/ms_nt/1e9:7.1f} TF | dX {ms_ntx*1e3:7.1f} us "
+              f"{f/ms_ntx/1e9:7.1f} TF", flush=True)
+        if n == 4 * k:   # FF Dense_0: GEMM + GELU (library + torch elementwise) vs the fused epilogue
+            bias = torch.zeros(n, device=dev)
+            hh = torch.randn(m, n, device=dev).to(torch.bfloat16)
+            ms_lg = bench(lambda: torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a, b), approximate="tanh"))
+            ms_ng = bench(lambda: ops.gemm_nt(a, bt, bias, ops.EPI_GELU))
+            dyk = torch.randn(m, k, device=dev).to(torch.bfloat16)
+            bk = torch.randn(n, k, device=dev).to(torch.bfloat16)   # Dense_1 kernel [hid, out]
+            ms_ld = bench(lambda: torch.ops.aten.gelu_backward(dyk @ bk.t(), hh, approximate="tanh"))
+            ms_nd = bench(lambda: ops.gemm_nt(dyk, bk, None, ops.EPI_DGELU, aux=hh))
+            print(f"{name:9s} Dense_0+GELU lib {ms_lg*1e3:7.1f} us fused {ms_ng*1e3:7.1f} us | "
+                  f"Dense_1 dX+GELU' lib {ms_ld*1e3:7.1f} us fused {ms_nd*1e3:7.1f} us", flush=True)
         print(f"{name:9s} M={m:6d} K={k:5d} N={n:5d} | fwd {ms*1e3:7.1f} us {f/ms/1e9:7.1f} TF | dX {ms_x*1e3:7.1f} us "
               f"{f/ms_x/1e9:7.1f} TF | dW lib {ms_w*1e3:7.1f} us {f/ms_w/1e9:7.1f} TF | dW+db hip {ms_h*1e3:7.1f} us "
               f"{f/ms_h/1e9:7.1f} TF", flush=True)
