@@ -639,8 +639,11 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const v
 
 // ------------------------------------------------------------------ projection gradients
 static void dw_plan(int M, int I, int J, int* S, int* chunk) {
+  // at most 512 workgroups = one resident round (2 per CU x 256 CUs): a 513th would run alone in
+  // a second round (the old ceil() rule launched 513 / 540 / 513 for the DeiT-S QKV / FF / output
+  // projections)
   const int tiles = ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
-  int s = (512 + tiles - 1) / tiles;
+  int s = 512 / tiles;
   s = std::max(1, std::min(s, (M + 255) / 256));
   int c = (M + s - 1) / s;
   c = (c + kDwK - 1) / kDwK * kDwK;

@@ -105,12 +105,13 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   }
   const unsigned xstep = (unsigned)(kDwK * a.ldx * 2), ystep = (unsigned)(kDwK * a.ldy * 2);
   const int nst = (m1 - m0 + kDwK - 1) / kDwK;
+  // straight-line staging (as gemm_nt.h): stage loads / LDS writes past the end are issued
+  // unconditionally (they read zeros: the descriptors end at m1) so the waitcnt pass keeps two
+  // register stages in flight instead of draining the queue before every reload
   xs[0].load(rx, 0);
   ys[0].load(ry, 0);
-  if (nst > 1) {
-    xs[1].load(rx, xstep);
-    ys[1].load(ry, ystep);
-  }
+  xs[1].load(rx, xstep);
+  ys[1].load(ry, ystep);
 
   unsigned ca[8];   // [operand x / dy][t = 0, 1][r1, r2] transposed-read addresses
   {
@@ -139,41 +140,40 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
+  auto compute = [&](const char* imx, const char* imy) {
+#pragma unroll
+    for (int k = 0; k < kDwK / 16; ++k) {
+      const bf16x8 a0 = dw_colfrag(imx, ca, k, 0), a1 = dw_colfrag(imx, ca, k, 1);
+      const bf16x8 b0 = dw_colfrag(imy, ca + 4, k, 0), b1 = dw_colfrag(imy, ca + 4, k, 1);
+      acc[0][0] = MF<__bf16>::mma(a0, b0, acc[0][0]);
+      acc[0][1] = MF<__bf16>::mma(a0, b1, acc[0][1]);
+      acc[1][0] = MF<__bf16>::mma(a1, b0, acc[1][0]);
+      acc[1][1] = MF<__bf16>::mma(a1, b1, acc[1][1]);
+      if (bias) {
+        accb[0] = MF<__bf16>::mma(ones, b0, accb[0]);
+        accb[1] = MF<__bf16>::mma(ones, b1, accb[1]);
+      }
+    }
+  };
   xs[0].write(smem);
   ys[0].write(smem + IMG);
   __syncthreads();
-  for (int st0 = 0; st0 < nst; st0 += 2) {
+  int st = 0;
+  for (; st + 2 <= nst; st += 2) {
 #pragma unroll
     for (int bsel = 0; bsel < 2; ++bsel) {
-      const int st = st0 + bsel;
-      if (st >= nst) break;
       const char* imx = smem + bsel * 2 * IMG;
-      const char* imy = imx + IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
-      if (st + 2 < nst) {   // register set bsel was written to LDS at the end of stage st - 1
-        xs[bsel].load(rx, (unsigned)(st + 2) * xstep);
-        ys[bsel].load(ry, (unsigned)(st + 2) * ystep);
-      }
-#pragma unroll
-      for (int k = 0; k < kDwK / 16; ++k) {
-        const bf16x8 a0 = dw_colfrag(imx, ca, k, 0), a1 = dw_colfrag(imx, ca, k, 1);
-        const bf16x8 b0 = dw_colfrag(imy, ca + 4, k, 0), b1 = dw_colfrag(imy, ca + 4, k, 1);
-        acc[0][0] = MF<__bf16>::mma(a0, b0, acc[0][0]);
-        acc[0][1] = MF<__bf16>::mma(a0, b1, acc[0][1]);
-        acc[1][0] = MF<__bf16>::mma(a1, b0, acc[1][0]);
-        acc[1][1] = MF<__bf16>::mma(a1, b1, acc[1][1]);
-        if (bias) {
-          accb[0] = MF<__bf16>::mma(ones, b0, accb[0]);
-          accb[1] = MF<__bf16>::mma(ones, b1, accb[1]);
-        }
-      }
-      if (st + 1 < nst) {
-        xs[bsel ^ 1].write(nxt);
-        ys[bsel ^ 1].write(nxt + IMG);
-      }
+      // register set bsel was written to LDS at the end of the previous stage: refill (stage + 2)
+      xs[bsel].load(rx, (unsigned)(st + bsel + 2) * xstep);
+      ys[bsel].load(ry, (unsigned)(st + bsel + 2) * ystep);
+      compute(imx, imx + IMG);
+      xs[bsel ^ 1].write(nxt);
+      ys[bsel ^ 1].write(nxt + IMG);
       __syncthreads();
     }
   }
+  if (st < nst) compute(smem, smem + IMG);   // odd stage count: the last stage sits in buffer 0
   // fp32 partial tile: accumulator row = i (row_of), column = j (lane)
   float* P = a.part + (size_t)s * a.I * a.J;
   const int jc = j0 + 64 * wj + (lane & 31);

@@ -103,11 +103,29 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
     bs[q].init(tid, a.ldb);
   }
   const int nst = a.K / kNtK;
+  // Straight-line staging (no data-dependent branches around the loads and LDS writes): the
+  // loads of stages st + 2 and the LDS writes of stage st + 1 are issued unconditionally --
+  // past the end they read zeros (descriptor range check) or unused bytes into a buffer nobody
+  // reads again -- so the waitcnt pass can prove each register set's loads retired and keeps two
+  // stages in flight (with conditional loads it waited vmcnt(0) before every reload).
   as[0].load(ra, 0);
   bs[0].load(rb, 0);
-  if (nst > 1) {
-    as[1].load(ra, kNtK * 2);
-    bs[1].load(rb, kNtK * 2);
+  as[1].load(ra, kNtK * 2);
+  bs[1].load(rb, kNtK * 2);
+  // kEpiDGelu: this lane's eight aux chunks (the epilogue's row groups) are loaded before the
+  // main loop, so their HBM traffic overlaps the MFMAs instead of following them
+  const int c8 = lane & 7;                 // 16-byte chunk of an epilogue row segment
+  const int n = n0 + 64 * wn + 8 * c8;     // its first feature
+  uint4 auxv[2][4];
+  if constexpr (EPI == kEpiDGelu) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int m = m0 + 64 * wm + 32 * u + 8 * it + (lane >> 3);
+        auxv[u][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n)
+                                           : uint4{0, 0, 0, 0};
+      }
   }
   f32x16 acc[2][2];   // [feature sub-tile t][token sub-tile u]
 #pragma unroll
@@ -115,39 +133,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) acc[t][u] = zero16();
 
+  auto compute = [&](const char* ima, const char* imb) {
+#pragma unroll
+    for (int s = 0; s < kNtK / 16; ++s) {
+      const bf16x8 b0 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + r, s, h);
+      const bf16x8 b1 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + 32 + r, s, h);
+      const bf16x8 a0 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + r, s, h);
+      const bf16x8 a1 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + 32 + r, s, h);
+      acc[0][0] = MF<__bf16>::mma(b0, a0, acc[0][0]);
+      acc[0][1] = MF<__bf16>::mma(b0, a1, acc[0][1]);
+      acc[1][0] = MF<__bf16>::mma(b1, a0, acc[1][0]);
+      acc[1][1] = MF<__bf16>::mma(b1, a1, acc[1][1]);
+    }
+  };
   as[0].write(smem);
   bs[0].write(smem + IMG);
   __syncthreads();
-  for (int st0 = 0; st0 < nst; st0 += 2) {
+  int st = 0;
+  for (; st + 2 <= nst; st += 2) {
 #pragma unroll
     for (int bsel = 0; bsel < 2; ++bsel) {
-      const int st = st0 + bsel;
-      if (st >= nst) break;
       const char* ima = smem + bsel * 2 * IMG;
-      const char* imb = ima + IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
-      if (st + 2 < nst) {   // register set bsel went to LDS at the end of stage st - 1
-        as[bsel].load(ra, (unsigned)(st + 2) * (kNtK * 2));
-        bs[bsel].load(rb, (unsigned)(st + 2) * (kNtK * 2));
-      }
-#pragma unroll
-      for (int s = 0; s < kNtK / 16; ++s) {
-        const bf16x8 b0 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + r, s, h);
-        const bf16x8 b1 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + 32 + r, s, h);
-        const bf16x8 a0 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + r, s, h);
-        const bf16x8 a1 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + 32 + r, s, h);
-        acc[0][0] = MF<__bf16>::mma(b0, a0, acc[0][0]);
-        acc[0][1] = MF<__bf16>::mma(b0, a1, acc[0][1]);
-        acc[1][0] = MF<__bf16>::mma(b1, a0, acc[1][0]);
-        acc[1][1] = MF<__bf16>::mma(b1, a1, acc[1][1]);
-      }
-      if (st + 1 < nst) {
-        as[bsel ^ 1].write(nxt);
-        bs[bsel ^ 1].write(nxt + IMG);
-      }
+      // register set bsel went to LDS at the end of the previous stage: refill it (stage + 2)
+      as[bsel].load(ra, (unsigned)(st + bsel + 2) * (kNtK * 2));
+      bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (kNtK * 2));
+      compute(ima, ima + IMG);
+      as[bsel ^ 1].write(nxt);
+      bs[bsel ^ 1].write(nxt + IMG);
       __syncthreads();
     }
   }
+  if (st < nst) compute(smem, smem + IMG);   // odd stage count: the last stage sits in buffer 0
 
   // ---- epilogue: accumulator row = feature nb + 32t + row_of(reg, h), column = token (lane)
   const int nb = n0 + 64 * wn;
@@ -168,8 +185,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   char* scratch = smem + w * (32 * 64 * 2);   // 4 KiB per wave; the stage buffers are free now
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
   typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
-  const int c8 = lane & 7;          // 16-byte chunk of the row segment (features nb + 8 c8 ..)
-  const int n = nb + 8 * c8;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -198,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
           *reinterpret_cast<bf16x8v*>(a.c + (long long)m * a.ldc + n) = y;
         } else {
           const bf16x8v dv = __builtin_bit_cast(bf16x8v, raw);
-          const bf16x8v hv = *reinterpret_cast<const bf16x8v*>(a.aux + (long long)m * a.ldaux + n);
+          const bf16x8v hv = __builtin_bit_cast(bf16x8v, auxv[u][it]);
           bf16x8v y;
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] = (__bf16)((float)dv[e] * dgelu_f((float)hv[e]));

@@ -493,12 +493,9 @@ class _FFBlock(torch.autograd.Function):
         if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
             x2 = x2.contiguous()
         w0p, w0t = weight_cast(w0)
-        w1p, _ = weight_cast(w1, transposed=False)
+        w1p, w1t = weight_cast(w1)
         a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
-        if use_gemm_nt(Hd):
-            y = gemm_nt(a, w1p.t().contiguous(), b1)
-        else:   # deep reduction (K = hidden): the library GEMM is faster there
-            y = torch.addmm(b1.to(torch.bfloat16), a, w1p) if b1 is not None else a @ w1p
+        y = gemm_nt(a, w1t, b1)   # K = hidden (1536): 42 vs 44 us for the library GEMM
         ctx.save_for_backward(x2, h, a, w0p, w1p)
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
         return y.view(*x.shape[:-1], w1.shape[1])
