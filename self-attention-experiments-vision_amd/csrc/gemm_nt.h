@@ -56,6 +56,36 @@ __device__ __forceinline__ float dgelu_f(float x) {
   return s + 2.f * x * s * (1.f - s) * (kGeluB + (3.f * kGeluB * kGeluK) * x * x);
 }
 
+// The epilogues on pairs of elements: the polynomial / sigmoid algebra in packed f32
+// (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: two elements per VALU issue), the two
+// transcendentals per element scalar.  A bf16 pair is one 32-bit word: lo = w << 16, hi = w & ~0xffff.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 bf2_to_f2(unsigned w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned f2_to_bf2(f32x2 v) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  const bf16x2 b = {(__bf16)v.x, (__bf16)v.y};
+  return __builtin_bit_cast(unsigned, b);
+}
+__device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {   // sigmoid(2y) of both elements
+  constexpr float c1 = -2.f * kLog2e * kGeluB, c2 = -2.f * kLog2e * kGeluB * kGeluK;
+  const f32x2 t = x * (c1 + c2 * (x * x));
+  const f32x2 d = f32x2{ex2(t.x), ex2(t.y)} + 1.f;
+  return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+__device__ __forceinline__ unsigned gelu_bf2(unsigned hw) {
+  const f32x2 x = bf2_to_f2(hw);
+  return f2_to_bf2(x * gelu_sig2(x));
+}
+__device__ __forceinline__ unsigned dgelu_bf2(unsigned dw, unsigned hw) {   // d * gelu'(h)
+  const f32x2 x = bf2_to_f2(hw);
+  const f32x2 s = gelu_sig2(x);
+  const f32x2 q = s - s * s;                                    // s (1 - s)
+  const f32x2 poly = (2.f * kGeluB) + (6.f * kGeluB * kGeluK) * (x * x);
+  return f2_to_bf2(bf2_to_f2(dw) * ((x * q) * poly + s));
+}
+
 // one operand's 128 x 64 stage: 1024 16-byte chunks, 4 per thread
 struct NtStage {
   uint4 v[4];
@@ -184,7 +214,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   }
   char* scratch = smem + w * (32 * 64 * 2);   // 4 KiB per wave; the stage buffers are free now
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -206,18 +235,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
           *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
         } else if constexpr (EPI == kEpiGelu) {
           *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
-          const bf16x8v hv = __builtin_bit_cast(bf16x8v, raw);
-          bf16x8v y;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = (__bf16)gelu_f((float)hv[e]);
-          *reinterpret_cast<bf16x8v*>(a.c + (long long)m * a.ldc + n) = y;
+          const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
+          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
         } else {
-          const bf16x8v dv = __builtin_bit_cast(bf16x8v, raw);
-          const bf16x8v hv = __builtin_bit_cast(bf16x8v, auxv[u][it]);
-          bf16x8v y;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = (__bf16)((float)dv[e] * dgelu_f((float)hv[e]));
-          *reinterpret_cast<bf16x8v*>(a.c + (long long)m * a.ldc + n) = y;
+          const uint4 hv = auxv[u][it];
+          const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
+                           dgelu_bf2(raw.w, hv.w)};
+          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
         }
       }
     }
