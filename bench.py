@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 METRIC = "attention fwd+bwd TFLOP/s (% MFMA peak); DeiT-S/16 train img/s at 1/8 GPUs"
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
+TIMER_STEPS = 3               # graph mode: eager steps timed with HIP events after the timed region
 RIDGE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
 
 
@@ -166,7 +167,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
-    ap.add_argument("--model", default="deit_s_patch16")
+    ap.add_argument("--model", default="deit_s_patch16",
+                    help="ViT/DeiT (vit.MODEL_CONFIGS) or CaiT (cait.CAIT_CONFIGS, e.g. cait_s_24: configs[4])")
+    ap.add_argument("--img-size", type=int, default=224,
+                    help="input resolution (384 with --model vit_b_patch16 --batch 32: BASELINE configs[2])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-headline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="training loop only (for rocprofv3 runs)")
@@ -176,7 +180,7 @@ def main():
     import torch
     import torch.distributed as dist
     import sae_vision_amd
-    from sae_vision_amd import ops, train, vit
+    from sae_vision_amd import cait, ops, train, vit
 
     rank, world, local = train.init_distributed()
     if world != args.gpus:
@@ -185,14 +189,18 @@ def main():
     sae_vision_amd.load_library()
 
     torch.manual_seed(0)
-    model = vit.create_model(args.model, 1000, torch.bfloat16, device=dev)
+    is_cait = args.model in cait.CAIT_CONFIGS
+    if is_cait:   # BASELINE configs[4]; stochastic depth at its config rate (a real training step)
+        model = cait.create_cait(args.model, 1000, torch.bfloat16, img_size=args.img_size, device=dev)
+    else:
+        model = vit.create_model(args.model, 1000, torch.bfloat16, img_size=args.img_size, device=dev)
     B = args.batch
     # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1: the
     # eager DDP step (RCCL all-reduce overlapped with the backward through DDP's bucket hooks)
     use_graph = world == 1 and not args.eager
     step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    images = torch.randn(B, 224, 224, 3, device=dev, generator=g)
+    images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
     labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
     for _ in range(args.warmup):
@@ -216,7 +224,7 @@ def main():
         # graph replays carry no host-side events: time the same kernels with HIP events on their
         # launch stream over eager steps of the same workload, right after the timed region
         ops.set_kernel_timer(timer)
-        for _ in range(3):
+        for _ in range(TIMER_STEPS):
             step._eager(images, labels)
         ops.set_kernel_timer(None)
     if world > 1:
@@ -226,14 +234,26 @@ def main():
     final_loss = float(loss.item())
 
     ksum = timer.summary()
-    L, Hh, C, p = vit.MODEL_CONFIGS[args.model]
-    N = (224 // p) ** 2 + 1
+    timed_steps = TIMER_STEPS if use_graph else args.steps
+    if is_cait:   # the dominant attention: the talking-heads self-attention trunk (no CLS token)
+        L, _, Hh, C, _, _ = cait.CAIT_CONFIGS[args.model]
+        N = (args.img_size // 16) ** 2
+        kf, kb = "th_attn_fwd", "th_attn_bwd"
+    else:
+        L, Hh, C, p = vit.MODEL_CONFIGS[args.model]
+        N = (args.img_size // p) ** 2 + 1
+        kf, kb = "attn_fwd", "attn_bwd"
     D = C // Hh
     f_fwd, f_bwd, b_fwd, b_bwd = attn_work(B, N, N, Hh, D)
-    fwd_ms, bwd_ms = ksum["attn_fwd"]["mean_ms"], ksum["attn_bwd"]["mean_ms"]
-    roof = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, (fwd_ms + bwd_ms) / 1e3, load_traffic("deit_s"))
+    if is_cait:   # + the two H x H head mixes, fwd and bwd
+        f_fwd += 2 * 2.0 * B * Hh * Hh * N * N
+        f_bwd += 2 * 4.0 * B * Hh * Hh * N * N
+    fwd_ms, bwd_ms = ksum[kf]["mean_ms"], ksum[kb]["mean_ms"]
+    roof = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, (fwd_ms + bwd_ms) / 1e3,
+                          load_traffic("deit_s") if (args.model, args.img_size) == ("deit_s_patch16", 224) else None)
     img_s = B * world * args.steps / elapsed
-    flop_img = 3 * vit.vit_flops_per_image(args.model)
+    flop_img = 3 * (cait.cait_flops_per_image(args.model, args.img_size) if is_cait
+                    else vit.vit_flops_per_image(args.model, args.img_size))
 
     if rank != 0:
         if world > 1:
@@ -243,14 +263,14 @@ def main():
         "metric": METRIC, "value": round(img_s, 2), "unit": "img/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": f"DeiT-S/16 224px bf16 data-parallel training step (fused attention fwd+bwd)",
+        "config": {"workload": f"{args.model} {args.img_size}px bf16 data-parallel training step (fused attention fwd+bwd)",
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "step": "hip_graph_replay" if use_graph else "eager"},
         "roofline": roof,
-        "attention": {"calls_per_step": ksum["attn_fwd"]["launches"] // args.steps, "fwd_ms": round(fwd_ms, 4),
-                      "bwd_ms": round(bwd_ms, 4), "tflops": roof["tflops"],
-                      "share_of_step": round((fwd_ms + bwd_ms) * ksum["attn_fwd"]["launches"] / args.steps
+        "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,
+                      "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4), "tflops": roof["tflops"],
+                      "share_of_step": round((fwd_ms + bwd_ms) * ksum[kf]["launches"] / timed_steps
                                              / (elapsed / args.steps * 1e3), 4)},
         "e2e": {"train_flop_per_img": flop_img, "tflops": round(img_s * flop_img / 1e12, 1),
                 "mfma_frac": round(img_s * flop_img / 1e12 / (world * PEAK_BF16_TFLOPS), 4),
@@ -258,7 +278,7 @@ def main():
     }
     if not args.profile and not args.no_headline:
         out["attention_headline"] = headline(dev)
-    if not args.profile and not args.no_cpu_baseline and world == 1:
+    if not args.profile and not args.no_cpu_baseline and world == 1 and args.img_size == 224 and not is_cait:
         out["cpu_baseline"] = cpu_baseline(args.model)
     print(json.dumps(out), flush=True)
     if world > 1:

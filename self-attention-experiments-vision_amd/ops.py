@@ -226,8 +226,11 @@ class _TalkingHeads(torch.autograd.Function):
         o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
         lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
         d = _make_desc(q, k, v, o, scale)
+        tok = _TIMER.begin("th_attn_fwd") if _TIMER is not None else None
         L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
                                     _ptr(th2c), _ptr(o), _ptr(lse)))
+        if tok is not None:
+            _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
         ctx.save_for_backward(q, k, v, th1c, th2c, lse)
         ctx.scale = scale
         ctx.th_dtypes = (th1.dtype, th2.dtype)
@@ -242,9 +245,12 @@ class _TalkingHeads(torch.autograd.Function):
         dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
         d = _make_desc(q, k, v, None, ctx.scale, do, dq, dk, dv)
         ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
+        tok = _TIMER.begin("th_attn_bwd") if _TIMER is not None else None
         L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
                                     _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
                                     _ptr(ws)))
+        if tok is not None:
+            _TIMER.end(tok, tuple(q.shape))
         return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
 
 

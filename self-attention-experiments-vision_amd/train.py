@@ -94,8 +94,15 @@ class TrainStep:
         torch.cuda.current_stream(images.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(g):
-            self._loss = self._eager(self._images, self._labels)
+        try:
+            with torch.cuda.graph(g):
+                self._loss = self._eager(self._images, self._labels)
+        except RuntimeError as e:   # an op that cannot be captured: stay eager, say so once
+            import sys
+            print(f"[train] HIP-graph capture failed ({e}); running the eager step", file=sys.stderr)
+            self.graph = False
+            torch.cuda.synchronize()
+            return
         self._g = g
 
     def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
@@ -103,6 +110,8 @@ class TrainStep:
             return self._eager(images, labels)
         if self._g is None:
             self._capture(images, labels)
+            if not self.graph:
+                return self._eager(images, labels)
         if images.data_ptr() != self._images.data_ptr():
             self._images.copy_(images)
         if labels.data_ptr() != self._labels.data_ptr():

@@ -1,0 +1,47 @@
+"""CaiT caller (models/cait.py) on CPU: the Flax parameter tree, LayerScale init and the
+stochastic-depth rule (stochastic_depth.py:6-28).  No kernels run here."""
+import torch
+
+
+def test_cait_param_tree_names():
+    from sae_vision_amd import cait
+    m = cait.CaiT(num_classes=10, num_layers=2, num_layers_token_only=2, num_heads=4, embed_dim=64,
+                  patch_shape=(16, 16), stoch_depth_rate=0.1, layerscale_eps=1e-5, img_size=32)
+    names = {n for n, _ in m.named_parameters()}
+    for want in ("PatchEmbedBlock_0.Dense_0.kernel", "cls", "Dense_0.kernel", "Dense_0.bias", "LayerNorm_0.scale",
+                 "Encoder_0.AddAbsPosEmbed_0.pos_embed",
+                 "Encoder_0.EncoderBlock_1.SelfAttentionBlock_0.queries.kernel",
+                 "Encoder_0.EncoderBlock_1.SelfAttentionBlock_0.TalkingHeadsBlock_0.talking_heads_transform",
+                 "Encoder_0.EncoderBlock_1.SelfAttentionBlock_0.TalkingHeadsBlock_1.talking_heads_transform",
+                 "Encoder_0.EncoderBlock_0.LayerScaleBlock_0.layerscale",
+                 "Encoder_0.EncoderBlock_0.LayerScaleBlock_1.layerscale",
+                 "Encoder_0.EncoderBlock_0.FFBlock_0.Dense_1.kernel",
+                 "CAEncoderBlock_1.ClassSelfAttentionBlock_0.DenseGeneral_0.kernel",
+                 "CAEncoderBlock_0.LayerScaleBlock_1.layerscale"):
+        assert want in names, want
+    assert m.Encoder_0.AddAbsPosEmbed_0.pos_embed.shape == (1, 4, 64)      # no CLS in the trunk
+    ls = m.Encoder_0.EncoderBlock_0.LayerScaleBlock_0.layerscale
+    assert torch.equal(ls, torch.full((64,), 1e-5))
+    assert float(m.Dense_0.kernel.abs().max()) == 0.0                       # zeros init (cait.py:183)
+
+
+def test_cait_configs_match_create_model():
+    from sae_vision_amd import cait
+    # create_model.py: cait_s_24 = 24 layers, 2 token-only, 8 heads, 384 dim, sd 0.1, eps 1e-6
+    assert cait.CAIT_CONFIGS["cait_s_24"] == (24, 2, 8, 384, 0.1, 1e-6)
+    assert abs(cait.cait_flops_per_image("cait_s_24") / 1e9 - 18.65) < 0.05     # ~18.6
+
+
+def test_stochastic_depth_rule():
+    from sae_vision_amd import cait
+    torch.manual_seed(0)
+    blk = cait.StochasticDepthBlock(0.3)
+    x = torch.ones(4000, 3, 5)
+    y = blk(x, is_training=True)
+    per = y[:, 0, 0]
+    kept = per != 0
+    assert torch.allclose(per[kept], torch.full_like(per[kept], 1 / 0.7))
+    assert torch.equal(y, per[:, None, None].expand_as(y))                 # one draw per sample
+    assert abs(float(kept.float().mean()) - 0.7) < 0.03
+    assert torch.equal(blk(x, is_training=False), x)
+    assert torch.equal(cait.StochasticDepthBlock(0.0)(x, is_training=True), x)
