@@ -60,6 +60,19 @@ class StochasticDepthBlock(nn.Module):
         return x / keep * mask.to(x.dtype)
 
 
+def scaled_branch(x: torch.Tensor, ls: LayerScaleBlock, sd: StochasticDepthBlock, dtype: torch.dtype,
+                  is_training: bool) -> torch.Tensor:
+    """``StochasticDepth(LayerScale(x))`` as ONE elementwise pass: x * (layerscale[c] * mask[b] /
+    keep), the [B, 1, C] factor built first (same math as the two blocks applied in turn,
+    layerscale.py:21-23 then stochastic_depth.py:19-28, up to the bf16 rounding of the factor)."""
+    f = ls.layerscale.to(dtype)
+    if is_training and sd.drop_rate > 0.0:
+        keep = 1.0 - sd.drop_rate
+        mask = torch.floor(keep + torch.rand((x.shape[0],), device=x.device, dtype=torch.float32)) / keep
+        f = f[None, None, :] * mask[:, None, None].to(dtype)
+    return x.to(dtype) * f
+
+
 class EncoderBlock(nn.Module):
     """cait.py:18-60: LN -> talking-heads SelfAttention -> LayerScale -> StochDepth -> + ;
     LN -> FF -> LayerScale -> StochDepth -> +."""
@@ -84,10 +97,10 @@ class EncoderBlock(nn.Module):
 
     def forward(self, inputs: torch.Tensor, is_training: bool) -> torch.Tensor:
         x = self.SelfAttentionBlock_0(self._ln(self.LayerNorm_0, inputs), is_training=is_training)
-        x = self.StochasticDepthBlock_0(self.LayerScaleBlock_0(x, self.dtype), is_training)
+        x = scaled_branch(x, self.LayerScaleBlock_0, self.StochasticDepthBlock_0, self.dtype, is_training)
         x = x + inputs                                         # fp32 residual stream
         y = self.FFBlock_0(self._ln(self.LayerNorm_1, x), self.dtype)
-        y = self.StochasticDepthBlock_1(self.LayerScaleBlock_1(y, self.dtype), is_training)
+        y = scaled_branch(y, self.LayerScaleBlock_1, self.StochasticDepthBlock_1, self.dtype, is_training)
         return x + y
 
 
@@ -106,8 +119,25 @@ class Encoder(nn.Module):
 
     def forward(self, inputs: torch.Tensor, is_training: bool) -> torch.Tensor:
         x = inputs.float() + self.AddAbsPosEmbed_0.pos_embed
-        for i in range(self.num_layers):
-            x = getattr(self, f"EncoderBlock_{i}")(x, is_training)
+        blocks = [getattr(self, f"EncoderBlock_{i}") for i in range(self.num_layers)]
+        if blocks and blocks[0].dtype == torch.bfloat16 and ops.layer_norm_ok(x):
+            # cait.py:30-60 per block, every residual add fused with the LayerNorm that follows it
+            # (this block's LayerNorm_1, the next block's LayerNorm_0): one HBM pass each
+            h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
+            for i, blk in enumerate(blocks):
+                a = blk.SelfAttentionBlock_0(h, is_training=is_training)
+                a = scaled_branch(a, blk.LayerScaleBlock_0, blk.StochasticDepthBlock_0, blk.dtype, is_training)
+                x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
+                f = blk.FFBlock_0(h, blk.dtype)
+                f = scaled_branch(f, blk.LayerScaleBlock_1, blk.StochasticDepthBlock_1, blk.dtype, is_training)
+                if i + 1 < len(blocks):
+                    nxt = blocks[i + 1].LayerNorm_0
+                    x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+                else:
+                    x = x + f
+            return x
+        for blk in blocks:
+            x = blk(x, is_training)
         return x
 
 
@@ -135,10 +165,10 @@ class CAEncoderBlock(nn.Module):
     def forward(self, inputs: torch.Tensor, cls_token: torch.Tensor, is_training: bool) -> torch.Tensor:
         x = torch.cat([cls_token, inputs], dim=1)
         x = self.ClassSelfAttentionBlock_0(self._ln(self.LayerNorm_0, x.contiguous()), is_training=is_training)
-        x = self.StochasticDepthBlock_0(self.LayerScaleBlock_0(x, self.dtype), is_training)
+        x = scaled_branch(x, self.LayerScaleBlock_0, self.StochasticDepthBlock_0, self.dtype, is_training)
         cls_token = cls_token + x
         y = self.FFBlock_0(self._ln(self.LayerNorm_1, cls_token.contiguous()), self.dtype)
-        y = self.StochasticDepthBlock_1(self.LayerScaleBlock_1(y, self.dtype), is_training)
+        y = scaled_branch(y, self.LayerScaleBlock_1, self.StochasticDepthBlock_1, self.dtype, is_training)
         return cls_token + y
 
 

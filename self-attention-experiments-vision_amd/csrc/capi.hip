@@ -311,7 +311,7 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
                   (sizeof(T) == 2 ? (size_t)a.H * 2 * Img<T, DP>::bytes(32) : 0);
   hipLaunchKernelGGL((th_bwd_kv_kernel<T, DP, VEC>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
   if (hipGetLastError() != hipSuccess) return 1;
-  hipLaunchKernelGGL(th_reduce_kernel, dim3((2 * a.H * a.H + 255) / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(th_reduce_kernel, dim3(2 * a.H * a.H), dim3(256), 0, st, a);
   return hipGetLastError() != hipSuccess;
 }
 

@@ -145,7 +145,10 @@ class AttentionBlock(nn.Module):
             k, v = kv[:, :, 0], kv[:, :, 1]
         if self.rotary:
             q, k = ops.rotary(q), ops.rotary(k)
-        if self.talking_heads:
+        if self.talking_heads and self_attn and not self.rotary:
+            o = ops.talking_heads_attention_packed(qkv, self.TalkingHeadsBlock_0.talking_heads_transform,
+                                                   self.TalkingHeadsBlock_1.talking_heads_transform, scale)
+        elif self.talking_heads:
             o = ops.talking_heads_attention(q, k, v, self.TalkingHeadsBlock_0.talking_heads_transform,
                                             self.TalkingHeadsBlock_1.talking_heads_transform, scale)
         elif self_attn and not self.rotary:

@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -215,22 +215,41 @@ def attention_packed(qkv: torch.Tensor, scale: Optional[float] = None) -> torch.
 
 
 # ----------------------------------------------------------------------------- talking heads
+def _th_fwd(q, k, v, th1, th2, scale):
+    lib = L.load()
+    B, Nq, H, D = q.shape
+    th1c = th1.detach().to(torch.float32).contiguous()
+    th2c = th2.detach().to(torch.float32).contiguous()
+    o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
+    d = _make_desc(q, k, v, o, scale)
+    tok = _TIMER.begin("th_attn_fwd") if _TIMER is not None else None
+    L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
+                                _ptr(th2c), _ptr(o), _ptr(lse)))
+    if tok is not None:
+        _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
+    return o, lse, th1c, th2c
+
+
+def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale):
+    lib = L.load()
+    dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
+    d = _make_desc(q, k, v, None, scale, do, dq, dk, dv)
+    ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
+    tok = _TIMER.begin("th_attn_bwd") if _TIMER is not None else None
+    L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
+                                _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
+                                _ptr(ws)))
+    if tok is not None:
+        _TIMER.end(tok, tuple(q.shape))
+    return dth1, dth2
+
+
 class _TalkingHeads(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, th1, th2, scale):
         _require_gpu(q, k, v, th1, th2)
-        lib = L.load()
-        B, Nq, H, D = q.shape
-        th1c = th1.detach().to(torch.float32).contiguous()
-        th2c = th2.detach().to(torch.float32).contiguous()
-        o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
-        lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
-        d = _make_desc(q, k, v, o, scale)
-        tok = _TIMER.begin("th_attn_fwd") if _TIMER is not None else None
-        L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
-                                    _ptr(th2c), _ptr(o), _ptr(lse)))
-        if tok is not None:
-            _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
+        o, lse, th1c, th2c = _th_fwd(q, k, v, th1, th2, scale)
         ctx.save_for_backward(q, k, v, th1c, th2c, lse)
         ctx.scale = scale
         ctx.th_dtypes = (th1.dtype, th2.dtype)
@@ -239,19 +258,42 @@ class _TalkingHeads(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, th1, th2, lse = ctx.saved_tensors
-        lib = L.load()
         do = _grad_in(do)
         dq, dk, dv = (torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in (q, k, v))
-        dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
-        d = _make_desc(q, k, v, None, ctx.scale, do, dq, dk, dv)
-        ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
-        tok = _TIMER.begin("th_attn_bwd") if _TIMER is not None else None
-        L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
-                                    _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
-                                    _ptr(ws)))
-        if tok is not None:
-            _TIMER.end(tok, tuple(q.shape))
+        dth1, dth2 = _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, ctx.scale)
         return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
+
+
+class _TalkingHeadsPacked(torch.autograd.Function):
+    """Talking heads on the packed projection [B, N, 3, H, D]: dq / dk / dv land in ONE gradient
+    buffer through strides (no per-view gradient accumulation passes)."""
+
+    @staticmethod
+    def forward(ctx, qkv, th1, th2, scale):
+        _require_gpu(qkv, th1, th2)
+        o, lse, th1c, th2c = _th_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, scale)
+        ctx.save_for_backward(qkv, th1c, th2c, lse)
+        ctx.scale = scale
+        ctx.th_dtypes = (th1.dtype, th2.dtype)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, th1, th2, lse = ctx.saved_tensors
+        do = _grad_in(do)
+        dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        dth1, dth2 = _th_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, lse, do, dqkv[:, :, 0],
+                             dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale)
+        return dqkv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
+
+
+def talking_heads_attention_packed(qkv, th1, th2, scale: Optional[float] = None):
+    """Talking-heads self-attention on a packed projection ``qkv`` [B, N, 3, H, D]."""
+    if qkv.dim() != 5 or qkv.shape[2] != 3:
+        raise ValueError(f"expected qkv [B, N, 3, H, D], got {tuple(qkv.shape)}")
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    return _TalkingHeadsPacked.apply(qkv, th1, th2, float(scale))
 
 
 def talking_heads_attention(q, k, v, th1, th2, scale: Optional[float] = None):

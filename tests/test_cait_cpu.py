@@ -45,3 +45,18 @@ def test_stochastic_depth_rule():
     assert abs(float(kept.float().mean()) - 0.7) < 0.03
     assert torch.equal(blk(x, is_training=False), x)
     assert torch.equal(cait.StochasticDepthBlock(0.0)(x, is_training=True), x)
+
+
+def test_scaled_branch_equals_layerscale_then_stochdepth():
+    from sae_vision_amd import cait
+    ls = cait.LayerScaleBlock(16, 0.5)
+    with torch.no_grad():
+        ls.layerscale.uniform_(0.1, 1.0)
+    sd = cait.StochasticDepthBlock(0.4)
+    x = torch.randn(64, 5, 16)
+    torch.manual_seed(3)
+    a = cait.scaled_branch(x, ls, sd, torch.float32, True)
+    torch.manual_seed(3)
+    b = sd(ls(x, torch.float32), True)
+    assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
+    assert torch.equal(cait.scaled_branch(x, ls, sd, torch.float32, False), ls(x, torch.float32))
