@@ -33,9 +33,13 @@ def init_distributed():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SAE_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin; gloo all-reduces the CUDA gradients through host memory)
+    backend = os.environ.get("SAE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     elif torch.cuda.is_available():
