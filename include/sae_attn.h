@@ -173,6 +173,17 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
 /* fp32 Dense kernel w [K][N] -> bf16 w16 [K][N] and/or its transpose wt16 [N][K] (either may
    be NULL): the compute-dtype casts of Flax Dense (kernel cast to dtype). */
 int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w16, void* wt16);
+/* Many casts in one launch (every Dense kernel of a model once per step): item i casts
+   w [K][N] (contiguous fp32) into columns col0 .. col0+N-1 of w16 [K][ld16] and rows
+   col0 .. col0+N-1 of wt16 [*][ldT] (either may be NULL) -- e.g. the queries / keys / values
+   kernels into one stacked [C][3HD] projection and its transpose. */
+typedef struct sae_weight_cast_item {
+  const float* w;
+  void* w16;
+  void* wt16;
+  int32_t K, N, ld16, ldT, col0;
+} sae_weight_cast_item;
+int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* items);
 
 /* Residual add + LayerNorm of the encoder blocks around the path (models/vit.py:19-31,57;
    Flax nn.LayerNorm: fp32 statistics, eps, output in the compute dtype):

@@ -56,6 +56,7 @@ _PROTOS = [
     ("sae_gemm_dw", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
     ("sae_gemm_nt", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
     ("sae_weight_cast", _i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    ("sae_weight_cast_multi", _i32, [_vp, _i32, _vp]),
     ("sae_layernorm_fwd", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32]),
     ("sae_layernorm_bwd_workspace_bytes", _sz, [_i32, _i32]),
     ("sae_layernorm_bwd", _i32, [_vp, _i32, _i32] + [_vp] * 11),
@@ -66,6 +67,13 @@ _PROTOS = [
 EXPORTED_SYMBOLS = [p[0] for p in _PROTOS]
 
 _lib = None
+
+
+class WeightCastItem(ctypes.Structure):
+    """Mirror of ``sae_weight_cast_item`` (include/sae_attn.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("w16", ctypes.c_void_p), ("wt16", ctypes.c_void_p),
+                ("K", ctypes.c_int32), ("N", ctypes.c_int32), ("ld16", ctypes.c_int32), ("ldT", ctypes.c_int32),
+                ("col0", ctypes.c_int32)]
 
 
 class SaeError(RuntimeError):

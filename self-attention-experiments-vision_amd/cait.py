@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from . import ops
 from .layers.attention import ClassSelfAttentionBlock, SelfAttentionBlock
-from .vit import Dense, FFBlock, LayerNorm
+from .vit import Dense, FFBlock, LayerNorm, encoder_weight_groups
 
 __all__ = ["CaiT", "create_cait", "CAIT_CONFIGS", "cait_flops_per_image", "LayerScaleBlock",
            "StochasticDepthBlock"]
@@ -123,21 +123,29 @@ class Encoder(nn.Module):
         if blocks and blocks[0].dtype == torch.bfloat16 and ops.layer_norm_ok(x):
             # cait.py:30-60 per block, every residual add fused with the LayerNorm that follows it
             # (this block's LayerNorm_1, the next block's LayerNorm_0): one HBM pass each
-            h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
-            for i, blk in enumerate(blocks):
-                a = blk.SelfAttentionBlock_0(h, is_training=is_training)
-                a = scaled_branch(a, blk.LayerScaleBlock_0, blk.StochasticDepthBlock_0, blk.dtype, is_training)
-                x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
-                f = blk.FFBlock_0(h, blk.dtype)
-                f = scaled_branch(f, blk.LayerScaleBlock_1, blk.StochasticDepthBlock_1, blk.dtype, is_training)
-                if i + 1 < len(blocks):
-                    nxt = blocks[i + 1].LayerNorm_0
-                    x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
-                else:
-                    x = x + f
-            return x
+            ops.cast_weights(encoder_weight_groups(blocks))   # every Dense kernel, one launch
+            try:
+                return self._fused(x, blocks, is_training)
+            finally:
+                ops.clear_weight_cache()
         for blk in blocks:
             x = blk(x, is_training)
+        return x
+
+    @staticmethod
+    def _fused(x, blocks, is_training):
+        h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
+        for i, blk in enumerate(blocks):
+            a = blk.SelfAttentionBlock_0(h, is_training=is_training)
+            a = scaled_branch(a, blk.LayerScaleBlock_0, blk.StochasticDepthBlock_0, blk.dtype, is_training)
+            x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
+            f = blk.FFBlock_0(h, blk.dtype)
+            f = scaled_branch(f, blk.LayerScaleBlock_1, blk.StochasticDepthBlock_1, blk.dtype, is_training)
+            if i + 1 < len(blocks):
+                nxt = blocks[i + 1].LayerNorm_0
+                x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+            else:
+                x = x + f
         return x
 
 

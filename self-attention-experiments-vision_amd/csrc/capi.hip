@@ -767,6 +767,39 @@ int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w1
   return check_launch("weight_cast");
 }
 
+int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* items) {
+  if (n < 0 || (n > 0 && !items)) return fail(SAE_EINVAL, "weight_cast_multi: bad item list");
+  hipStream_t st = (hipStream_t)stream;
+  for (int base = 0; base < n; base += kCastMax) {
+    CastList L;
+    memset(&L, 0, sizeof L);
+    L.n = std::min(kCastMax, n - base);
+    long long tiles = 0;
+    for (int j = 0; j < L.n; ++j) {
+      const sae_weight_cast_item& s = items[base + j];
+      if (!s.w || s.K < 1 || s.N < 1 || (!s.w16 && !s.wt16) || s.col0 < 0 ||
+          (s.w16 && s.ld16 < s.col0 + s.N) || (s.wt16 && s.ldT < s.K))
+        return fail(SAE_EINVAL, "weight_cast_multi: item %d invalid (K %d N %d ld16 %d ldT %d col0 %d)", base + j,
+                    s.K, s.N, s.ld16, s.ldT, s.col0);
+      CastItem& c = L.it[j];
+      c.w = s.w;
+      c.w16 = reinterpret_cast<__bf16*>(s.w16);
+      c.wt16 = reinterpret_cast<__bf16*>(s.wt16);
+      c.K = s.K;
+      c.N = s.N;
+      c.ld16 = s.ld16;
+      c.ldT = s.ldT;
+      c.col0 = s.col0;
+      c.tiles = ((s.K + 31) / 32) * ((s.N + 31) / 32);
+      tiles += c.tiles;
+    }
+    if (tiles >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "weight_cast_multi: too many tiles");
+    hipLaunchKernelGGL(weight_cast_multi_kernel, dim3((unsigned)tiles), dim3(256), 0, st, L);
+    if (int rc = check_launch("weight_cast_multi")) return rc;
+  }
+  return ok();
+}
+
 // ------------------------------------------------------------ residual add + LayerNorm
 static int ln_fwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 2048)); }
 static int ln_bwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 1024)); }

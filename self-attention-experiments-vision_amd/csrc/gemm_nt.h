@@ -277,4 +277,49 @@ __global__ __launch_bounds__(256) void weight_cast_kernel(const float* w, __bf16
   }
 }
 
+// Every Dense kernel of a model cast in ONE launch (the per-weight casts are ~4 us each, almost
+// all launch / ramp latency): item i casts w_i [K][N] into columns col0 .. col0 + N of
+// w16 [K][ld16] and rows col0 .. col0 + N of wt16 [*][ldT]; 32 x 32 tiles, items located by a
+// prefix sum over their tile counts.
+constexpr int kCastMax = 48;
+struct CastItem {
+  const float* w;
+  __bf16* w16;
+  __bf16* wt16;
+  int K, N, ld16, ldT, col0, tiles;
+};
+struct CastList {
+  CastItem it[kCastMax];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void weight_cast_multi_kernel(CastList L) {
+  __shared__ float tile[32][33];
+  int b = blockIdx.x, i = 0;
+  while (i + 1 < L.n && b >= L.it[i].tiles) b -= L.it[i++].tiles;
+  const CastItem& c = L.it[i];
+  const int tn = (c.N + 31) / 32;
+  const int k0 = (b / tn) * 32, n0 = (b % tn) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = k0 + ty + 8 * r, n = n0 + tx;
+    v[r] = (k < c.K && n < c.N) ? c.w[(long long)k * c.N + n] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = k0 + ty + 8 * r, n = n0 + tx;
+    if (c.w16 && k < c.K && n < c.N) c.w16[(long long)k * c.ld16 + c.col0 + n] = (__bf16)v[r];
+    tile[ty + 8 * r][tx] = v[r];
+  }
+  if (!c.wt16) return;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int n = n0 + ty + 8 * r, k = k0 + tx;
+    if (k < c.K && n < c.N) c.wt16[(long long)(c.col0 + n) * c.ldT + k] = (__bf16)tile[tx][ty + 8 * r];
+  }
+}
+
 }  // namespace sae

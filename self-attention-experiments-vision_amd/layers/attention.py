@@ -107,6 +107,14 @@ class AttentionBlock(nn.Module):
             self.TalkingHeadsBlock_1 = TalkingHeadsBlock(H, device)
         self.DenseGeneral_0 = DenseGeneral((H, head_ch), (out_ch,), self.use_bias, device)
 
+    def weight_groups(self):
+        """The fp32 kernels as the 2-D column blocks the projections use (``ops.cast_weights``)."""
+        if self._in_ch is None:
+            return []
+        C, HD = self._in_ch, self.num_heads * self._head_ch_eff
+        return [[m.kernel.reshape(C, HD) for m in (self.queries, self.keys, self.values)],
+                [self.DenseGeneral_0.kernel.reshape(HD, self._out_ch_eff)]]
+
     # -- forward -----------------------------------------------------------------------
     def forward(self, inputs_q: torch.Tensor, inputs_kv: torch.Tensor, is_training: bool) -> torch.Tensor:
         assert inputs_q.ndim == inputs_kv.ndim == 3
@@ -132,7 +140,7 @@ class AttentionBlock(nn.Module):
         self_attn = inputs_q is inputs_kv
         if self_attn:
             # ONE projection GEMM producing the packed [B, N, 3, H, D] buffer the kernels read in place
-            w = torch.stack((wq, wk, wv), dim=1).reshape(C, 3 * HD)
+            w = [wq.reshape(C, HD), wk.reshape(C, HD), wv.reshape(C, HD)]   # = stack(dim=1) columns
             qkv = ops.dense(xq, w, bias(self.queries, self.keys, self.values) if bias else None, dt)
             qkv = qkv.view(B, Nq, 3, H, D)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
@@ -140,7 +148,7 @@ class AttentionBlock(nn.Module):
             xkv = inputs_kv.to(dt)
             q = ops.dense(xq, wq.reshape(C, HD), self.queries.bias.reshape(-1) if bias else None, dt)
             q = q.view(B, Nq, H, D)
-            kv = ops.dense(xkv, torch.stack((wk, wv), dim=1).reshape(C, 2 * HD),
+            kv = ops.dense(xkv, [wk.reshape(C, HD), wv.reshape(C, HD)],
                            bias(self.keys, self.values) if bias else None, dt).view(B, Nk, 2, H, D)
             k, v = kv[:, :, 0], kv[:, :, 1]
         if self.rotary:

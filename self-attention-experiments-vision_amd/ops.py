@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "cast_weights", "clear_weight_cache", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -426,24 +426,85 @@ def _dw_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
             and x2.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0)
 
 
+# ----------------------------------------------------- per-forward cache of the bf16 weight casts
+# ``cast_weights`` casts every Dense kernel of an encoder in ONE launch (sae_weight_cast_multi) at
+# the start of its forward; the projections look their casts up while that forward runs and the
+# encoder clears the cache when it returns (nothing outlives the forward: the next optimizer step
+# changes the fp32 weights).  Keys are the fp32 weights' data pointers, checked with versions.
+_WCACHE = {}
+
+
+def _wkey(ws):
+    return tuple(w.data_ptr() for w in ws)
+
+
+def cast_weights(groups) -> None:
+    """``groups``: lists of fp32 2-D weights [K, n_j] (same K) stacked along columns; each group
+    gets a bf16 [K, sum n_j] and its transpose, cached under the group's key."""
+    lib = L.load()
+    items = []
+    dev = None
+    for ws in groups:
+        K = ws[0].shape[0]
+        if any(w.dim() != 2 or w.shape[0] != K or w.dtype != torch.float32 or not w.is_contiguous() for w in ws):
+            continue
+        dev = ws[0].device
+        N = sum(w.shape[1] for w in ws)
+        w16 = torch.empty((K, N), dtype=torch.bfloat16, device=dev)
+        wt16 = torch.empty((N, K), dtype=torch.bfloat16, device=dev)
+        col = 0
+        for w in ws:
+            items.append(L.WeightCastItem(w.data_ptr(), w16.data_ptr(), wt16.data_ptr(), K, w.shape[1], N, K, col))
+            col += w.shape[1]
+        _WCACHE[_wkey(ws)] = (tuple(w._version for w in ws), w16, wt16)
+    if items:
+        arr = (L.WeightCastItem * len(items))(*items)
+        L.check(lib.sae_weight_cast_multi(_stream(groups[0][0]), len(items), arr))
+
+
+def clear_weight_cache() -> None:
+    _WCACHE.clear()
+
+
+def _cast_lookup(ws):
+    e = _WCACHE.get(_wkey(ws))
+    if e is not None and e[0] == tuple(w._version for w in ws):
+        return e[1], e[2]
+    return None
+
+
+def _cast(ws, dt):
+    """bf16 [K, N] and [N, K] of the column-stacked fp32 weights ``ws`` (cached, or one launch)."""
+    hit = _cast_lookup(ws) if dt == torch.bfloat16 else None
+    if hit is not None:
+        return hit
+    w = ws[0] if len(ws) == 1 else torch.cat(ws, dim=1)
+    if dt == torch.bfloat16 and w.dtype == torch.float32 and w.is_cuda:
+        return weight_cast(w)
+    return w.to(dt), None
+
+
 class _Dense(torch.autograd.Function):
     """y = x @ W (+ b): Flax ``Dense`` / ``DenseGeneral`` semantics (input and fp32 kernel cast to
-    the compute dtype).  Backward: dX = dY W^T (library GEMM), dW / db straight into fp32 by the
-    split-token MFMA kernel (``sae_gemm_dw``) when the compute dtype is bf16."""
+    the compute dtype).  ``W`` may be given as column blocks (the queries / keys / values kernels of
+    one stacked projection): their gradients come back as the matching column slices.  Backward:
+    dX = dY W^T, dW / db straight into fp32 by the split-token MFMA kernel (``sae_gemm_dw``) when
+    the compute dtype is bf16."""
 
     @staticmethod
-    def forward(ctx, x, w, b, dt):
-        I, J = w.shape
+    def forward(ctx, x, b, dt, *ws):
+        I = ws[0].shape[0]
+        J = sum(w.shape[1] for w in ws)
         x2 = x.to(dt).reshape(-1, I)
-        if dt == torch.bfloat16 and w.dtype == torch.float32 and use_gemm_nt(I) and _nt_ok(x2, J):
-            wd, wt = weight_cast(w)                       # both layouts in one pass
+        wd, wt = _cast(ws, dt)
+        if wt is not None and use_gemm_nt(I) and _nt_ok(x2, J):
             y = gemm_nt(x2, wt, b)                        # bias in the epilogue
         else:
-            wd = w.to(dt)
             # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
             y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
         ctx.save_for_backward(x2, wd)
-        ctx.has_b, ctx.xshape, ctx.wdtype, ctx.xdtype = b is not None, x.shape, w.dtype, x.dtype
+        ctx.has_b, ctx.xshape, ctx.xdtype = b is not None, x.shape, x.dtype
+        ctx.wmeta = [(w.shape[1], w.dtype) for w in ws]
         return y.view(*x.shape[:-1], J)
 
     @staticmethod
@@ -461,16 +522,21 @@ class _Dense(torch.autograd.Function):
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
             gemm_dw(x2, dy2, dw, db)
-            dw = dw.to(ctx.wdtype)
         else:
-            dw = (x2.t() @ dy2).to(ctx.wdtype)
+            dw = (x2.t() @ dy2).float()
             db = dy2.sum(0, dtype=torch.float32) if ctx.has_b else None
-        return dx, dw, db, None
+        dws, col = [], 0
+        for n, wdt in ctx.wmeta:
+            dws.append(dw[:, col:col + n].to(wdt))
+            col += n
+        return (dx, db, None, *dws)
 
 
-def dense(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
-    """Projection of the hot path: ``x @ w (+ b)`` in ``dtype`` with fp32 parameter gradients."""
-    return _Dense.apply(x, w, b, dtype)
+def dense(x: torch.Tensor, w, b: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
+    """Projection of the hot path: ``x @ w (+ b)`` in ``dtype`` with fp32 parameter gradients.
+    ``w`` is a 2-D kernel [in, out] or a list of them stacked along the output axis."""
+    ws = list(w) if isinstance(w, (list, tuple)) else [w]
+    return _Dense.apply(x, b, dtype, *ws)
 
 
 # ------------------------------------------------- forward / input-gradient GEMMs (sae_gemm_nt)
@@ -540,8 +606,8 @@ class _FFBlock(torch.autograd.Function):
         x2 = x.to(torch.bfloat16).reshape(-1, I)
         if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
             x2 = x2.contiguous()
-        w0p, w0t = weight_cast(w0)
-        w1p, w1t = weight_cast(w1)
+        w0p, w0t = _cast([w0], torch.bfloat16)
+        w1p, w1t = _cast([w1], torch.bfloat16)
         a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
         y = gemm_nt(a, w1t, b1)   # K = hidden (1536): 42 vs 44 us for the library GEMM
         ctx.save_for_backward(x2, h, a, w0p, w1p)

@@ -92,6 +92,16 @@ class EncoderBlock(nn.Module):
         return x + y
 
 
+def encoder_weight_groups(blocks):
+    """Column-block groups of every Dense kernel of the blocks (attention QKV / output projection,
+    FF Dense_0 / Dense_1) for ``ops.cast_weights``."""
+    groups = []
+    for blk in blocks:
+        groups += blk.SelfAttentionBlock_0.weight_groups()
+        groups += [[blk.FFBlock_0.Dense_0.kernel], [blk.FFBlock_0.Dense_1.kernel]]
+    return groups
+
+
 class Encoder(nn.Module):
     """vit.py:35-58 (AddAbsPosEmbed_0 + EncoderBlock_i + LayerNorm_0)."""
 
@@ -110,14 +120,19 @@ class Encoder(nn.Module):
         blocks = [getattr(self, f"EncoderBlock_{i}") for i in range(self.num_layers)]
         if self.dtype == torch.bfloat16 and blocks and ops.layer_norm_ok(x):
             # Same math as vit.py:19-31,57, with every residual add fused into the LayerNorm that
-            # follows it (the next block's LayerNorm_0, or the final one): one HBM pass each.
-            h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
-            for i, blk in enumerate(blocks):
-                a = blk.SelfAttentionBlock_0(h, is_training=is_training)
-                x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
-                f = blk.FFBlock_0(h, self.dtype)
-                nxt = blocks[i + 1].LayerNorm_0 if i + 1 < len(blocks) else self.LayerNorm_0
-                x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+            # follows it (the next block's LayerNorm_0, or the final one): one HBM pass each; every
+            # Dense kernel of the encoder cast to bf16 in one launch up front.
+            ops.cast_weights(encoder_weight_groups(blocks))
+            try:
+                h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
+                for i, blk in enumerate(blocks):
+                    a = blk.SelfAttentionBlock_0(h, is_training=is_training)
+                    x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
+                    f = blk.FFBlock_0(h, self.dtype)
+                    nxt = blocks[i + 1].LayerNorm_0 if i + 1 < len(blocks) else self.LayerNorm_0
+                    x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+            finally:
+                ops.clear_weight_cache()
             return h
         for blk in blocks:
             x = blk(x, is_training)

@@ -153,3 +153,29 @@ def test_ff_block_deterministic(dev):
         outs.append([y.detach(), xx.grad] + [p.grad for p in ps])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_cast_weights_multi_exact(dev):
+    """sae_weight_cast_multi: column-stacked groups (queries / keys / values kernels into one
+    [C, 3HD] projection) in one launch, bit-equal to torch's casts; cache lookups and clearing."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(21)
+    C, H, D = 384, 6, 64
+    wq, wk, wv = (torch.randn(C, H, D, device=dev, generator=g) for _ in range(3))
+    wo = torch.randn(H, D, C, device=dev, generator=g)
+    ws = [[w.reshape(C, H * D) for w in (wq, wk, wv)], [wo.reshape(H * D, C)]]
+    ws += [[torch.randn(96, 40, device=dev, generator=g)] for _ in range(60)]   # > one launch of items
+    ops.cast_weights(ws)
+    try:
+        w16, wt16 = ops._cast_lookup(ws[0])
+        ref = torch.stack((wq, wk, wv), dim=1).reshape(C, 3 * H * D)
+        assert torch.equal(w16, ref.to(torch.bfloat16))
+        assert torch.equal(wt16, ref.t().contiguous().to(torch.bfloat16))
+        for grp in ws[1:]:
+            a, b = ops._cast_lookup(grp)
+            assert torch.equal(a, grp[0].to(torch.bfloat16)) and torch.equal(b, grp[0].t().to(torch.bfloat16))
+        wq.add_(1.0)                                   # in-place update: the entry is stale
+        assert ops._cast_lookup(ws[0]) is None
+    finally:
+        ops.clear_weight_cache()
+    assert ops._cast_lookup(ws[1]) is None
