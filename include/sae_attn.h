@@ -153,6 +153,12 @@ size_t sae_gemm_dw_workspace_bytes(int32_t M, int32_t I, int32_t J);
 int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx,
                 const void* dy, int64_t ldy, float* dw, int64_t ldw, float* db,
                 int32_t accumulate, void* workspace);
+/* Same, with dw laid out as J / jblock contiguous column blocks [J/jblock][I][jblock] (the
+   separate queries / keys / values kernel gradients of one stacked projection); jblock a
+   multiple of 4 dividing J.  Workspace: sae_gemm_dw_workspace_bytes(M, I, J). */
+int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t jblock,
+                        const void* x, int64_t ldx, const void* dy, int64_t ldy, float* dw,
+                        float* db, int32_t accumulate, void* workspace);
 
 /* Forward and input-gradient GEMMs of the projections and the FF block (the dot_generals of
    Flax Dense / DenseGeneral, attention.py:29-37,60-63 and ff.py:8-34), with the FF block's

@@ -54,6 +54,7 @@ _PROTOS = [
     ("sae_th_attn_bwd", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 13),
     ("sae_gemm_dw_workspace_bytes", _sz, [_i32, _i32, _i32]),
     ("sae_gemm_dw", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
+    ("sae_gemm_dw_blocked", _i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
     ("sae_gemm_nt", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
     ("sae_weight_cast", _i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
     ("sae_weight_cast_multi", _i32, [_vp, _i32, _vp]),

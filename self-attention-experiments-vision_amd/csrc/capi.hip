@@ -658,8 +658,25 @@ size_t sae_gemm_dw_workspace_bytes(int32_t M, int32_t I, int32_t J) {
   return (((size_t)S * I * J * 4 + 255) & ~(size_t)255) + (((size_t)S * J * 4 + 255) & ~(size_t)255);
 }
 
+static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx, const void* dy,
+                        int64_t ldy, float* dw, int64_t ldw, float* db, int32_t accumulate, void* workspace,
+                        int32_t jblock);
+
 int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx, const void* dy,
                 int64_t ldy, float* dw, int64_t ldw, float* db, int32_t accumulate, void* workspace) {
+  return gemm_dw_impl(stream, M, I, J, x, ldx, dy, ldy, dw, ldw, db, accumulate, workspace, 0);
+}
+
+int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t jblock, const void* x, int64_t ldx,
+                        const void* dy, int64_t ldy, float* dw, float* db, int32_t accumulate, void* workspace) {
+  if (jblock < 4 || jblock % 4 || J % jblock)
+    return fail(SAE_EINVAL, "gemm_dw_blocked: jblock (%d) must be a multiple of 4 dividing J (%d)", jblock, J);
+  return gemm_dw_impl(stream, M, I, J, x, ldx, dy, ldy, dw, J, db, accumulate, workspace, jblock);
+}
+
+static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const void* x, int64_t ldx, const void* dy,
+                        int64_t ldy, float* dw, int64_t ldw, float* db, int32_t accumulate, void* workspace,
+                        int32_t jblock) {
   if (M < 1 || I < 1 || J < 1) return fail(SAE_EINVAL, "gemm_dw: M/I/J must be >= 1 (got %d/%d/%d)", M, I, J);
   if (I % 8 || J % 8) return fail(SAE_EUNSUPPORTED, "gemm_dw: I (%d) and J (%d) must be multiples of 8", I, J);
   if (ldx < I || ldy < J || ldw < J || ldx % 8 || ldy % 8 || ldw % 4)
@@ -687,6 +704,7 @@ int sae_gemm_dw(void* stream, int32_t M, int32_t I, int32_t J, const void* x, in
   a.ldy = ldy;
   a.ldw = ldw;
   a.accumulate = accumulate;
+  a.jblock = jblock;
   hipStream_t st = (hipStream_t)stream;
   const long long grid = (long long)a.S * ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
   const size_t lds = 4 * kDwK * 256;

@@ -32,6 +32,7 @@ struct DwArgs {
   int M, I, J, S, chunk;   // chunk = tokens per split (multiple of 64)
   long long ldx, ldy, ldw;
   int accumulate;     // dw / db += instead of =
+  int jblock;         // > 0: dw is [J / jblock][I][jblock] (column blocks contiguous), ldw unused
 };
 
 constexpr int kDwT = 128;   // output tile edge
@@ -207,7 +208,9 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce_kernel(DwArgs a) {
       f32x4 acc = *reinterpret_cast<const f32x4*>(a.part + 4 * e);
       for (int s = 1; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(a.part + s * stride + 4 * e);
       const long long i = (4 * e) / a.J, j = (4 * e) % a.J;
-      f32x4* out = reinterpret_cast<f32x4*>(a.dw + i * a.ldw + j);
+      f32x4* out = reinterpret_cast<f32x4*>(
+          a.jblock ? a.dw + (j / a.jblock) * ((long long)a.I * a.jblock) + i * a.jblock + j % a.jblock
+                   : a.dw + i * a.ldw + j);
       if (a.accumulate) acc += *out;
       *out = acc;
     }

@@ -405,17 +405,22 @@ def rotary(x: torch.Tensor, base: float = 10000.0) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------ projections
 def gemm_dw(x2: torch.Tensor, dy2: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor] = None,
-            accumulate: bool = False) -> None:
+            accumulate: bool = False, jblock: int = 0) -> None:
     """dw (+)= x2^T dy2 and db (+)= colsum(dy2) in fp32 through ``sae_gemm_dw`` (split over the
-    token axis, fixed-order reduction).  x2 [M, I], dy2 [M, J] bf16 with unit column stride."""
+    token axis, fixed-order reduction).  x2 [M, I], dy2 [M, J] bf16 with unit column stride.
+    ``jblock`` > 0: dw is [J / jblock, I, jblock] (contiguous column blocks)."""
     lib = L.load()
     _require_gpu(x2, dy2, dw)
     M, I = x2.shape
     J = dy2.shape[1]
     ws = torch.empty(lib.sae_gemm_dw_workspace_bytes(M, I, J), dtype=torch.uint8, device=x2.device)
     tok = _TIMER.begin("gemm_dw") if _TIMER is not None else None
-    L.check(lib.sae_gemm_dw(_stream(x2), M, I, J, _ptr(x2), x2.stride(0), _ptr(dy2), dy2.stride(0), _ptr(dw),
-                            dw.stride(0), _ptr(db), int(accumulate), _ptr(ws)))
+    if jblock:
+        L.check(lib.sae_gemm_dw_blocked(_stream(x2), M, I, J, int(jblock), _ptr(x2), x2.stride(0), _ptr(dy2),
+                                        dy2.stride(0), _ptr(dw), _ptr(db), int(accumulate), _ptr(ws)))
+    else:
+        L.check(lib.sae_gemm_dw(_stream(x2), M, I, J, _ptr(x2), x2.stride(0), _ptr(dy2), dy2.stride(0), _ptr(dw),
+                                dw.stride(0), _ptr(db), int(accumulate), _ptr(ws)))
     if tok is not None:
         _TIMER.end(tok, (M, I, J))
 
@@ -518,7 +523,17 @@ class _Dense(torch.autograd.Function):
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
         else:
             dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
-        if _dw_ok(x2, dy2):
+        widths = [n for n, _ in ctx.wmeta]
+        blocked = len(widths) > 1 and len(set(widths)) == 1 and widths[0] % 4 == 0
+        if _dw_ok(x2, dy2) and (blocked or len(widths) == 1):
+            db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
+            if blocked:   # one contiguous [I, n] gradient per column block: no slice copies
+                dwb = torch.empty((len(widths), I, widths[0]), dtype=torch.float32, device=x2.device)
+                gemm_dw(x2, dy2, dwb, db, jblock=widths[0])
+                return (dx, db, None, *[dwb[k].to(wdt) for k, (_, wdt) in enumerate(ctx.wmeta)])
+            dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
+            gemm_dw(x2, dy2, dw, db)
+        elif _dw_ok(x2, dy2):
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
             gemm_dw(x2, dy2, dw, db)

@@ -82,3 +82,21 @@ def test_dense_grads_match_autograd(dev):
     ref_x = dy.double() @ wd.t()
     assert float((x.grad.double() - ref_x).abs().max() / ref_x.abs().max()) <= 2e-2
 
+
+
+def test_gemm_dw_blocked_layout(dev):
+    """sae_gemm_dw_blocked: dW in contiguous column blocks [J/jb, I, jb] equals the plain layout."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(17)
+    M, I, J, jb = 3000, 384, 1152, 384
+    x = torch.randn(M, I, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, J, device=dev, generator=g).to(torch.bfloat16)
+    dw = torch.empty(I, J, device=dev)
+    db = torch.empty(J, device=dev)
+    ops.gemm_dw(x, dy, dw, db)
+    dwb = torch.empty(J // jb, I, jb, device=dev)
+    db2 = torch.empty(J, device=dev)
+    ops.gemm_dw(x, dy, dwb, db2, jblock=jb)
+    for k in range(J // jb):
+        assert torch.equal(dwb[k], dw[:, k * jb:(k + 1) * jb])
+    assert torch.equal(db, db2)
