@@ -199,12 +199,27 @@ int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* i
 int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const void* delta,
                       float* xout, const float* gamma, const float* beta, void* y, float* mean,
                       float* rstd, float eps);
+/* CaiT form (layerscale.py:21-23, stochastic_depth.py:19-28 folded into the residual add):
+     xout = x + delta * layerscale[c] * rowscale[row / rows_per_sample]   (rowscale may be NULL)
+   layerscale fp32 [C] (16-byte aligned), rowscale fp32 [M / rows_per_sample]. */
+int sae_layernorm_fwd_scaled(void* stream, int32_t M, int32_t C, const float* x, const void* delta,
+                             float* xout, const float* gamma, const float* beta, void* y,
+                             float* mean, float* rstd, float eps, const float* layerscale,
+                             const float* rowscale, int32_t rows_per_sample);
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C);
 /* dx = dxin + dLN/dx(dy) (fp32; dxin may be NULL), ddelta = bf16(dx) (may be NULL),
    dgamma / dbeta fp32 [C] overwritten (fixed-order reduction, deterministic). */
 int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const float* mean,
                       const float* rstd, const float* gamma, const void* dy, const float* dxin,
                       float* dx, void* ddelta, float* dgamma, float* dbeta, void* workspace);
+/* Backward of the scaled form: ddelta = bf16(dx * layerscale * rowscale), dlayerscale[c] =
+   sum over rows of dx * delta * rowscale (fixed order, with dgamma / dbeta); delta is the bf16
+   addend of the forward. */
+int sae_layernorm_bwd_scaled(void* stream, int32_t M, int32_t C, const float* x, const float* mean,
+                             const float* rstd, const float* gamma, const void* dy, const float* dxin,
+                             float* dx, void* ddelta, float* dgamma, float* dbeta, void* workspace,
+                             const void* delta, const float* layerscale, const float* rowscale,
+                             int32_t rows_per_sample, float* dlayerscale);
 
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);

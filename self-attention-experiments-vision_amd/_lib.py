@@ -61,6 +61,9 @@ _PROTOS = [
     ("sae_layernorm_fwd", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32]),
     ("sae_layernorm_bwd_workspace_bytes", _sz, [_i32, _i32]),
     ("sae_layernorm_bwd", _i32, [_vp, _i32, _i32] + [_vp] * 11),
+    ("sae_layernorm_fwd_scaled", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp,
+                                        _i32]),
+    ("sae_layernorm_bwd_scaled", _i32, [_vp, _i32, _i32] + [_vp] * 14 + [_i32, _vp]),
     ("sae_last_error", ctypes.c_char_p, []),
     ("sae_abi_version", _i32, []),
     ("sae_build_info", ctypes.c_char_p, []),

@@ -66,11 +66,19 @@ def scaled_branch(x: torch.Tensor, ls: LayerScaleBlock, sd: StochasticDepthBlock
     keep), the [B, 1, C] factor built first (same math as the two blocks applied in turn,
     layerscale.py:21-23 then stochastic_depth.py:19-28, up to the bf16 rounding of the factor)."""
     f = ls.layerscale.to(dtype)
-    if is_training and sd.drop_rate > 0.0:
-        keep = 1.0 - sd.drop_rate
-        mask = torch.floor(keep + torch.rand((x.shape[0],), device=x.device, dtype=torch.float32)) / keep
-        f = f[None, None, :] * mask[:, None, None].to(dtype)
+    rs = sample_scale(x.shape[0], sd, is_training, x.device)
+    if rs is not None:
+        f = f[None, None, :] * rs[:, None, None].to(dtype)
     return x.to(dtype) * f
+
+
+def sample_scale(batch: int, sd: StochasticDepthBlock, is_training: bool, device):
+    """Per-sample stochastic-depth factor floor(keep + U[0,1)) / keep (stochastic_depth.py:19-28),
+    or None when the block is the identity."""
+    if not is_training or sd.drop_rate == 0.0:
+        return None
+    keep = 1.0 - sd.drop_rate
+    return torch.floor(keep + torch.rand((batch,), device=device, dtype=torch.float32)) / keep
 
 
 class EncoderBlock(nn.Module):
@@ -136,16 +144,18 @@ class Encoder(nn.Module):
     def _fused(x, blocks, is_training):
         h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
         for i, blk in enumerate(blocks):
+            # LayerScale x stochastic depth folded into the residual add + LayerNorm kernel
             a = blk.SelfAttentionBlock_0(h, is_training=is_training)
-            a = scaled_branch(a, blk.LayerScaleBlock_0, blk.StochasticDepthBlock_0, blk.dtype, is_training)
-            x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
+            rs = sample_scale(x.shape[0], blk.StochasticDepthBlock_0, is_training, x.device)
+            x, h = ops.add_layer_norm_scaled(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias,
+                                             blk.LayerScaleBlock_0.layerscale, rs)
             f = blk.FFBlock_0(h, blk.dtype)
-            f = scaled_branch(f, blk.LayerScaleBlock_1, blk.StochasticDepthBlock_1, blk.dtype, is_training)
             if i + 1 < len(blocks):
                 nxt = blocks[i + 1].LayerNorm_0
-                x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+                rs = sample_scale(x.shape[0], blk.StochasticDepthBlock_1, is_training, x.device)
+                x, h = ops.add_layer_norm_scaled(x, f, nxt.scale, nxt.bias, blk.LayerScaleBlock_1.layerscale, rs)
             else:
-                x = x + f
+                x = x + scaled_branch(f, blk.LayerScaleBlock_1, blk.StochasticDepthBlock_1, blk.dtype, is_training)
         return x
 
 

@@ -829,8 +829,29 @@ static int ln_check(int32_t M, int32_t C) {
   return SAE_OK;
 }
 
+static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const void* delta, float* xout,
+                       const float* gamma, const float* beta, void* y, float* mean, float* rstd, float eps,
+                       const float* lsc, const float* rsc, int32_t rpb);
+
 int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const void* delta, float* xout,
                       const float* gamma, const float* beta, void* y, float* mean, float* rstd, float eps) {
+  return ln_fwd_impl(stream, M, C, x, delta, xout, gamma, beta, y, mean, rstd, eps, nullptr, nullptr, 1);
+}
+
+int sae_layernorm_fwd_scaled(void* stream, int32_t M, int32_t C, const float* x, const void* delta, float* xout,
+                             const float* gamma, const float* beta, void* y, float* mean, float* rstd, float eps,
+                             const float* layerscale, const float* rowscale, int32_t rows_per_sample) {
+  if (!delta || !layerscale) return fail(SAE_EINVAL, "layernorm_fwd_scaled: delta and layerscale are required");
+  if (rowscale && (rows_per_sample < 1 || M % rows_per_sample))
+    return fail(SAE_EINVAL, "layernorm_fwd_scaled: rows_per_sample (%d) must divide M (%d)", rows_per_sample, M);
+  if (!aligned16(layerscale)) return fail(SAE_EINVAL, "layernorm_fwd_scaled: layerscale needs 16-byte alignment");
+  return ln_fwd_impl(stream, M, C, x, delta, xout, gamma, beta, y, mean, rstd, eps, layerscale, rowscale,
+                     rows_per_sample);
+}
+
+static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const void* delta, float* xout,
+                       const float* gamma, const float* beta, void* y, float* mean, float* rstd, float eps,
+                       const float* lsc, const float* rsc, int32_t rpb) {
   if (int rc = ln_check(M, C)) return rc;
   if (!x || !gamma || !beta || !y || !mean || !rstd) return fail(SAE_EINVAL, "layernorm_fwd: NULL argument");
   if ((delta == nullptr) != (xout == nullptr))
@@ -851,6 +872,9 @@ int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const 
   a.M = M;
   a.C = C;
   a.eps = eps;
+  a.lsc = lsc;
+  a.rsc = rsc;
+  a.rpb = rpb > 0 ? rpb : 1;
   const int nv = (C / 4 + 63) / 64;
   const dim3 g(ln_fwd_blocks(M)), b(256);
   hipStream_t st = (hipStream_t)stream;
@@ -865,12 +889,40 @@ int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const 
 
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
   if (M < 1 || C < 1) return 0;
-  return ((size_t)ln_bwd_blocks(M) + kLnSplit) * 2 * C * sizeof(float);
+  return ((size_t)ln_bwd_blocks(M) + kLnSplit) * 3 * C * sizeof(float);   // room for the scaled form
 }
+
+static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, const void* dy, const float* dxin, float* dx, void* ddelta,
+                       float* dgamma, float* dbeta, void* workspace, const void* delta, const float* lsc,
+                       const float* rsc, int32_t rpb, float* dlsc);
 
 int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
                       const float* gamma, const void* dy, const float* dxin, float* dx, void* ddelta, float* dgamma,
                       float* dbeta, void* workspace) {
+  return ln_bwd_impl(stream, M, C, x, mean, rstd, gamma, dy, dxin, dx, ddelta, dgamma, dbeta, workspace, nullptr,
+                     nullptr, nullptr, 1, nullptr);
+}
+
+int sae_layernorm_bwd_scaled(void* stream, int32_t M, int32_t C, const float* x, const float* mean,
+                             const float* rstd, const float* gamma, const void* dy, const float* dxin, float* dx,
+                             void* ddelta, float* dgamma, float* dbeta, void* workspace, const void* delta,
+                             const float* layerscale, const float* rowscale, int32_t rows_per_sample,
+                             float* dlayerscale) {
+  if (!delta || !layerscale || !dlayerscale)
+    return fail(SAE_EINVAL, "layernorm_bwd_scaled: delta, layerscale and dlayerscale are required");
+  if (rowscale && (rows_per_sample < 1 || M % rows_per_sample))
+    return fail(SAE_EINVAL, "layernorm_bwd_scaled: rows_per_sample (%d) must divide M (%d)", rows_per_sample, M);
+  if (!aligned16(layerscale) || ((uintptr_t)delta & 7))
+    return fail(SAE_EINVAL, "layernorm_bwd_scaled: layerscale needs 16-byte, delta 8-byte alignment");
+  return ln_bwd_impl(stream, M, C, x, mean, rstd, gamma, dy, dxin, dx, ddelta, dgamma, dbeta, workspace, delta,
+                     layerscale, rowscale, rows_per_sample, dlayerscale);
+}
+
+static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, const void* dy, const float* dxin, float* dx, void* ddelta,
+                       float* dgamma, float* dbeta, void* workspace, const void* delta, const float* lsc,
+                       const float* rsc, int32_t rpb, float* dlsc) {
   if (int rc = ln_check(M, C)) return rc;
   if (!x || !mean || !rstd || !gamma || !dy || !dx || !dgamma || !dbeta || !workspace)
     return fail(SAE_EINVAL, "layernorm_bwd: NULL argument");
@@ -893,22 +945,41 @@ int sae_layernorm_bwd(void* stream, int32_t M, int32_t C, const float* x, const 
   a.M = M;
   a.C = C;
   a.nblk = ln_bwd_blocks(M);
+  a.delta = reinterpret_cast<const __bf16*>(delta);
+  a.lsc = lsc;
+  a.rsc = rsc;
+  a.rpb = rpb > 0 ? rpb : 1;
+  a.dlsc = dlsc;
   const int nv = (C / 4 + 63) / 64;
   const dim3 g(a.nblk), b(256);
   hipStream_t st = (hipStream_t)stream;
+  const bool sc = lsc != nullptr;
+  const int np = sc ? 3 : 2;
+#define LNB(NV)                                                                \
+  if (sc) hipLaunchKernelGGL((ln_bwd_kernel<NV, 3>), g, b, 0, st, a);          \
+  else hipLaunchKernelGGL((ln_bwd_kernel<NV, 2>), g, b, 0, st, a);
   switch (nv) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, g, b, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, g, b, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, g, b, 0, st, a); break;
+    case 1: LNB(1) break;
+    case 2: LNB(2) break;
+    case 3: LNB(3) break;
+    default: LNB(4) break;
   }
+#undef LNB
   if (int rc = check_launch("layernorm_bwd")) return rc;
-  float* part2 = a.part + (size_t)a.nblk * 2 * C;
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
-                     (const float*)a.part, a.nblk, part2);
-  if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
-                     kLnSplit, (float*)nullptr);
+  float* part2 = a.part + (size_t)a.nblk * np * C;
+  if (sc) {
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
+                       (const float*)a.part, a.nblk, part2);
+    if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
+                       kLnSplit, (float*)nullptr);
+  } else {
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
+                       (const float*)a.part, a.nblk, part2);
+    if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
+                       kLnSplit, (float*)nullptr);
+  }
   return check_launch("layernorm_bwd_reduce2");
 }
 

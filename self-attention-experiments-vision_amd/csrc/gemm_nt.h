@@ -194,7 +194,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
       __syncthreads();
     }
   }
-  if (st < nst) compute(smem, smem + IMG);   // odd stage count: the last stage sits in buffer 0
+  if (st < nst) {   // odd stage count: the last stage sits in buffer 0
+    compute(smem, smem + IMG);
+    __syncthreads();   // every wave done with buffer 0 before the epilogue reuses it as scratch
+  }
 
   // ---- epilogue: accumulator row = feature nb + 32t + row_of(reg, h), column = token (lane)
   const int nb = n0 + 64 * wn;

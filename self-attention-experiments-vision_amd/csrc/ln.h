@@ -33,6 +33,12 @@ struct LnArgs {
   float* part;           // [nblk][2][C] per-workgroup dscale / dbias partials
   float* dgamma;         // [C]
   float* dbeta;          // [C]
+  // CaiT branch scale (layerscale.py:21-23 x stochastic_depth.py:19-28) folded into the add:
+  // x_out = x + delta * lsc[c] * rsc[row / rpb]   (lsc, rsc may be null = 1)
+  const float* lsc;      // [C] LayerScale parameter
+  const float* rsc;      // [M / rpb] per-sample stochastic-depth factor (mask / keep)
+  float* dlsc;           // [C] gradient of lsc (backward; needs delta)
+  int rpb;               // rows per sample
   int M, C, nblk;
   float eps;
 };
@@ -69,9 +75,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
     g[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.gamma)[c] : f32x4{};
     bt[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.beta)[c] : f32x4{};
   }
+  f32x4 ls[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = lane + 64 * k;
+    ls[k] = (a.lsc && c < C4) ? reinterpret_cast<const f32x4*>(a.lsc)[c] : f32x4{1.f, 1.f, 1.f, 1.f};
+  }
   const float invC = 1.f / (float)a.C;
   for (int row = wave; row < a.M; row += nw) {
     const size_t ro = (size_t)row * a.C;
+    const float rsf = a.rsc ? a.rsc[row / a.rpb] : 1.f;
     f32x4 v[NV];
     float s = 0.f;
 #pragma unroll
@@ -81,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
       if (c < C4) {
         v[k] = reinterpret_cast<const f32x4*>(a.x + ro)[c];
         if (a.delta) {
-          v[k] += ld_bf16x4(a.delta + ro + 4 * c);
+          v[k] += ld_bf16x4(a.delta + ro + 4 * c) * (ls[k] * rsf);
           reinterpret_cast<f32x4*>(a.xout + ro)[c] = v[k];
         }
       }
@@ -110,24 +123,27 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   }
 }
 
-template <int NV>
+// NP = 2: dgamma / dbeta partials; NP = 3: also the LayerScale gradient (a.lsc, a.delta set)
+template <int NV, int NP = 2>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
-  __shared__ f32x4 red[4][2][64 * NV];
+  __shared__ f32x4 red[4][NP][64 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wave = blockIdx.x * 4 + w;
   const int nw = gridDim.x * 4;
   const int C4 = a.C >> 2;
-  f32x4 g[NV], pg[NV], pb[NV];
+  f32x4 g[NV], pg[NV], pb[NV], pl[NV], ls[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = lane + 64 * k;
     g[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.gamma)[c] : f32x4{};
-    pg[k] = pb[k] = f32x4{};
+    ls[k] = (NP == 3 && c < C4) ? reinterpret_cast<const f32x4*>(a.lsc)[c] : f32x4{1.f, 1.f, 1.f, 1.f};
+    pg[k] = pb[k] = pl[k] = f32x4{};
   }
   const float invC = 1.f / (float)a.C;
   for (int row = wave; row < a.M; row += nw) {
     const size_t ro = (size_t)row * a.C;
     const float mu = a.mean[row], rs = a.rstd[row];
+    const float rsf = (NP == 3 && a.rsc) ? a.rsc[row / a.rpb] : 1.f;
     f32x4 xh[NV], gy[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -153,7 +169,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
         f32x4 d = (gy[k] - m1 - xh[k] * m2) * rs;
         if (a.dxin) d += reinterpret_cast<const f32x4*>(a.dxin + ro)[c];
         reinterpret_cast<f32x4*>(a.dx + ro)[c] = d;
-        if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d);
+        if constexpr (NP == 3) {   // x_out = x + delta * ls * rsf
+          pl[k] += d * ld_bf16x4(a.delta + ro + 4 * c) * rsf;
+          if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d * ls[k] * rsf);
+        } else {
+          if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d);
+        }
       }
     }
   }
@@ -162,15 +183,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
   for (int k = 0; k < NV; ++k) {
     red[w][0][lane + 64 * k] = pg[k];
     red[w][1][lane + 64 * k] = pb[k];
+    if constexpr (NP == 3) red[w][2][lane + 64 * k] = pl[k];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C4; i += 256) {
+  for (int i = threadIdx.x; i < NP * C4; i += 256) {
     const int which = i / C4, c = i % C4;
     f32x4 s = red[0][which][c];
     s += red[1][which][c];
     s += red[2][which][c];
     s += red[3][which][c];
-    reinterpret_cast<f32x4*>(a.part + ((size_t)blockIdx.x * 2 + which) * a.C)[c] = s;
+    reinterpret_cast<f32x4*>(a.part + ((size_t)blockIdx.x * NP + which) * a.C)[c] = s;
   }
 }
 
@@ -180,32 +202,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
 // strided groups, group sums in order); the final pass (gridDim.y == 1, nblk == kLnSplit, reading
 // part2) writes dgamma / dbeta.
 constexpr int kLnSplit = 16;
+template <int NP = 2>
 __global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a, const float* src, int nsrc, float* dst) {
-  __shared__ float red[4][2][64];
+  __shared__ float red[4][NP][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int per = (nsrc + gridDim.y - 1) / gridDim.y;
   const int b0 = blockIdx.y * per, b1 = min(nsrc, b0 + per);
-  float sg = 0.f, sb = 0.f;
+  float sum[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) sum[j] = 0.f;
   if (c < a.C) {
 #pragma unroll 4
     for (int b = b0 + grp; b < b1; b += 4) {
-      sg += src[((size_t)b * 2) * a.C + c];
-      sb += src[((size_t)b * 2 + 1) * a.C + c];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) sum[j] += src[((size_t)b * NP + j) * a.C + c];
     }
   }
-  red[grp][0][cl] = sg;
-  red[grp][1][cl] = sb;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) red[grp][j][cl] = sum[j];
   __syncthreads();
   if (grp == 0 && c < a.C) {
-    const float g = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-    const float bb = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
-    if (dst) {
-      dst[((size_t)blockIdx.y * 2) * a.C + c] = g;
-      dst[((size_t)blockIdx.y * 2 + 1) * a.C + c] = bb;
-    } else {
-      a.dgamma[c] = g;
-      a.dbeta[c] = bb;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const float t = ((red[0][j][cl] + red[1][j][cl]) + red[2][j][cl]) + red[3][j][cl];
+      if (dst) dst[((size_t)blockIdx.y * NP + j) * a.C + c] = t;
+      else (j == 0 ? a.dgamma : j == 1 ? a.dbeta : a.dlsc)[c] = t;
     }
   }
 }

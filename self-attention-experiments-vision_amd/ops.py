@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "cast_weights", "clear_weight_cache", "gemm_dw", "layer_norm", "add_layer_norm", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "cast_weights", "clear_weight_cache", "gemm_dw", "layer_norm", "add_layer_norm", "add_layer_norm_scaled", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -736,6 +736,62 @@ class _AddLayerNorm(torch.autograd.Function):
             dy = torch.zeros(xout.shape, dtype=torch.bfloat16, device=xout.device)
         dx, ddelta, dg, db = _ln_bwd(xout, mean, rstd, gamma, dy, dxout, True)
         return dx, ddelta.to(ctx.delta_dtype), dg, db, None
+
+
+class _AddLayerNormScaled(torch.autograd.Function):
+    """x + delta * layerscale[c] * rowscale[sample] and its LayerNorm (CaiT blocks)."""
+
+    @staticmethod
+    def forward(ctx, x, delta, gamma, beta, ls, rowscale, rpb, eps):
+        lib = L.load()
+        C = x.shape[-1]
+        M = x.numel() // C
+        delta = delta.contiguous()
+        # the reference casts the LayerScale parameter to the compute dtype (layerscale.py:22)
+        lsf = ls.detach().to(delta.dtype).float().contiguous()
+        y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+        xout = torch.empty_like(x)
+        L.check(lib.sae_layernorm_fwd_scaled(_stream(x), M, C, _ptr(x), _ptr(delta), _ptr(xout), _ptr(gamma),
+                                             _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), float(eps), _ptr(lsf),
+                                             _ptr(rowscale), int(rpb)))
+        ctx.save_for_backward(xout, mean, rstd, gamma, delta, lsf, rowscale)
+        ctx.rpb, ctx.delta_dtype, ctx.ls_dtype = int(rpb), delta.dtype, ls.dtype
+        return xout, y
+
+    @staticmethod
+    def backward(ctx, dxout, dy):
+        xout, mean, rstd, gamma, delta, lsf, rowscale = ctx.saved_tensors
+        lib = L.load()
+        C = xout.shape[-1]
+        M = xout.numel() // C
+        if dy is None:
+            dy = torch.zeros(xout.shape, dtype=torch.bfloat16, device=xout.device)
+        dy = dy.contiguous()
+        dxin = dxout.contiguous() if dxout is not None else None
+        dx = torch.empty_like(xout)
+        ddelta = torch.empty(xout.shape, dtype=torch.bfloat16, device=xout.device)
+        dg = torch.empty(C, dtype=torch.float32, device=xout.device)
+        db = torch.empty(C, dtype=torch.float32, device=xout.device)
+        dls = torch.empty(C, dtype=torch.float32, device=xout.device)
+        ws = torch.empty(lib.sae_layernorm_bwd_workspace_bytes(M, C), dtype=torch.uint8, device=xout.device)
+        L.check(lib.sae_layernorm_bwd_scaled(_stream(xout), M, C, _ptr(xout), _ptr(mean), _ptr(rstd), _ptr(gamma),
+                                             _ptr(dy), _ptr(dxin), _ptr(dx), _ptr(ddelta), _ptr(dg), _ptr(db),
+                                             _ptr(ws), _ptr(delta), _ptr(lsf), _ptr(rowscale), ctx.rpb, _ptr(dls)))
+        return dx, ddelta.to(ctx.delta_dtype), dg, db, dls.to(ctx.ls_dtype), None, None, None
+
+
+def add_layer_norm_scaled(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                          layerscale: torch.Tensor, rowscale: Optional[torch.Tensor] = None,
+                          eps: float = LN_EPS):
+    """CaiT residual add ``x + delta * layerscale * rowscale[sample]`` (layerscale.py:21-23 and the
+    stochastic-depth factor mask / keep, stochastic_depth.py:19-28) with its LayerNorm, one kernel;
+    returns ``(x_out, LN(x_out))``.  ``rowscale`` [B] fp32 or None; x [B, N, C] fp32."""
+    _require_gpu(x, delta)
+    if rowscale is not None:
+        rowscale = rowscale.float().contiguous()
+    return _AddLayerNormScaled.apply(x, delta, gamma, beta, layerscale, rowscale, x.shape[1], eps)
 
 
 def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = LN_EPS) -> torch.Tensor:

@@ -6,6 +6,7 @@ so y is checked at the bf16 bar (2e-2 of max|ref|); x + delta, dx and dscale / d
 sums of the same bf16 inputs and are checked at 1e-5."""
 import numpy as np
 import pytest
+import torch
 
 import vit_ref
 from _util import rel_err
@@ -88,3 +89,44 @@ def test_vit_train_grads_vs_oracle(dev):
     for k, p in m.named_parameters():
         err = rel_err(p.grad, grads_ref[k])
         assert err <= 6e-2, f"{k}: rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("rowscale", [False, True])
+def test_add_layer_norm_scaled(dev, rowscale):
+    """CaiT form: x + delta * bf16(layerscale) * rowscale[sample], LayerNorm, and every gradient
+    against float64 autograd of the same math (layerscale.py:21-23, stochastic_depth.py:19-28)."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(31)
+    B, N, C = 6, 196, 384
+    x = torch.randn(B, N, C, device=dev, generator=g)
+    delta = torch.randn(B, N, C, device=dev, generator=g).to(torch.bfloat16)
+    gamma = torch.rand(C, device=dev, generator=g) + 0.5
+    beta = torch.randn(C, device=dev, generator=g) * 0.1
+    ls = torch.rand(C, device=dev, generator=g) + 0.1
+    rs = torch.tensor([0.0, 1.25, 1.25, 0.0, 1.25, 1.25], device=dev) if rowscale else None
+    dxo = torch.randn(B, N, C, device=dev, generator=g)
+    dy = torch.randn(B, N, C, device=dev, generator=g).to(torch.bfloat16)
+
+    leaves = [t.clone().requires_grad_(True) for t in (x, gamma, beta, ls)]
+    d_leaf = delta.clone().requires_grad_(True)
+    xo, y = ops.add_layer_norm_scaled(leaves[0], d_leaf, leaves[1], leaves[2], leaves[3], rs)
+    torch.autograd.backward([xo, y], [dxo, dy])
+
+    r = [t.clone().double().requires_grad_(True) for t in (x, gamma, beta, ls)]
+    rd = delta.clone().double().requires_grad_(True)
+    f = r[3].detach().to(torch.bfloat16).double() + (r[3] - r[3].detach())   # bf16 value, identity gradient
+    if rs is not None:
+        f = f[None, None, :] * rs.double()[:, None, None]
+    xr = r[0] + rd * f
+    mu = xr.mean(-1, keepdim=True)
+    var = ((xr - mu) ** 2).mean(-1, keepdim=True)
+    yr = (xr - mu) / torch.sqrt(var + 1e-6) * r[1] + r[2]
+    torch.autograd.backward([xr, yr], [dxo.double(), dy.double()])
+    rel = lambda a, b: float((a.double() - b).abs().max() / b.abs().max().clamp_min(1e-30))
+    assert rel(xo, xr) <= 1e-6
+    assert rel(y, yr) <= 1e-2
+    assert rel(leaves[0].grad, r[0].grad) <= 1e-5
+    assert rel(d_leaf.grad, rd.grad) <= 1e-2
+    for got, want, name in ((leaves[1].grad, r[1].grad, "gamma"), (leaves[2].grad, r[2].grad, "beta"),
+                            (leaves[3].grad, r[3].grad, "layerscale")):
+        assert rel(got, want) <= 1e-4, name
