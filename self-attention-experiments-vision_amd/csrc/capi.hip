@@ -199,6 +199,11 @@ template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) 
     case 9: if constexpr (DP <= 64) return fwd3_run<DP, 4, 2, false>(st, a); else break;
     default: break;
   }
+  // long key ranges at D <= 64: three waves per SIMD, row sum on the VALU (variant 6) is 2.5 %
+  // faster at N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt);
+  // at D = 128 it is 2x slower
+  if constexpr (DP <= 64)
+    if (var == 0 && a.Nk >= 512) return fwd2_run<DP, 4, 3, false>(st, a);
   return fwd2_run<DP, 4, 2, true>(st, a);
 }
 
