@@ -14,7 +14,8 @@ from typing import Sequence
 import torch  # noqa: F401  (loads torch's libamdhip64.so.7 first so the library binds to the same HIP runtime)
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG_DIR, "libsae_attn.so")
+# SAE_ATTN_LIB points the tools at the development build (build.py --dev); default: release
+LIB_PATH = os.environ.get("SAE_ATTN_LIB") or os.path.join(_PKG_DIR, "libsae_attn.so")
 
 SAE_OK, SAE_EINVAL, SAE_EUNSUPPORTED, SAE_EHIP = 0, -1, -2, -3
 SAE_DTYPE_F32, SAE_DTYPE_BF16 = 0, 1

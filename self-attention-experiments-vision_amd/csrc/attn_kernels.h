@@ -36,6 +36,7 @@ struct AttnArgs {
   void* dk;
   void* dv;
   float* delta;     // bwd workspace [B, H, Nq]
+  float* dqp;       // bwd3 workspace: per-key-block dQ partials [nkb][B, H, Nq, DP] (fp32)
   const float* bias_h;
   const float* bias_w;
   float* dbias_h;
@@ -44,8 +45,6 @@ struct AttnArgs {
   long long qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
   float scale;
   int rel_h, rel_w, rel_magic;
-  int dbg;          // development knob (SAE_DBG): 0 in production
-  unsigned long long* dbgbuf;  // SAE_DBG & 64: per-workgroup timestamps (diagnostic builds only)
 };
 
 constexpr int kBQ = 128;   // query rows per forward / dq workgroup (4 waves x 32)
@@ -264,7 +263,6 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   using I = Img<T, DP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // double-buffered query tile: [buf][Q img | dO img | -lse/scale [64] | -delta [64] | REL bias [64][RW]]
-  wg_stamp(a.dbgbuf, a.dbg, 0);
   const int RW = a.rel_h + a.rel_w + 1;
   const int TB = 2 * I::bytes(kBQT) + 2 * kBQT * 4 + (REL ? kBQT * RW * 4 : 0);
 
@@ -354,7 +352,6 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   };
   put(smem, 0);
   __syncthreads();
-  wg_stamp(a.dbgbuf, a.dbg, 1);
 
   for (int qt = 0; qt < nqt; ++qt) {
     const char* ldsQ = smem + (nbuf<T, DP>() == 2 ? (qt & 1) : 0) * TB;
@@ -363,7 +360,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
     const float* ldsD = ldsL + kBQT;
     const float* ldsB = ldsD + kBQT;
     const bool more = qt + 1 < nqt;
-    if (more && !(a.dbg & 1)) {
+    if (more) {
       fetch_rc(qt + 1);
       if constexpr (VEC) {
         qst.load_buf(rq, (qt + 1) * kBQT, a.qs[1], a.D, tid);
@@ -373,7 +370,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         gst.load(G, (qt + 1) * kBQT, a.Nq, a.dos[1], a.D, tid);
       }
     }
-    const int nu = (!active || (a.dbg & 2)) ? 0 : (qt * kBQT + 32 < a.Nq ? 2 : 1);   // skip padding halves / idle waves
+    const int nu = !active ? 0 : (qt * kBQT + 32 < a.Nq ? 2 : 1);   // skip padding halves / idle waves
 #pragma unroll 1
     for (int u = 0; u < nu; ++u) {
       // row constants as the initial accumulators: S - lse/scale and dP - delta
@@ -423,9 +420,8 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
     __syncthreads();
   }
 
-  wg_stamp(a.dbgbuf, a.dbg, 2);
   if constexpr (sizeof(T) == 2 && VEC) {
-    if (active && !(a.dbg & 8)) {   // whole-row stores through a per-wave LDS scratch (buffers free)
+    if (active) {   // whole-row stores through a per-wave LDS scratch (buffers free)
       const int k0 = kb * kBKV + w * 32;
       char* scr = smem + w * 32 * DP * 2;
       T* DK = reinterpret_cast<T*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)k0 * a.dks[1];
@@ -433,7 +429,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
       wave_store_rows<DP>(adk, a.scale, scr, reinterpret_cast<__bf16*>(DK), a.dks[1], a.Nk - k0, a.D, lane);
       wave_store_rows<DP>(adv, 1.f, scr, reinterpret_cast<__bf16*>(DV), a.dvs[1], a.Nk - k0, a.D, lane);
     }
-  } else if (key < a.Nk && !(a.dbg & 8)) {
+  } else if (key < a.Nk) {
     T* DK = reinterpret_cast<T*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)key * a.dks[1];
     T* DV = reinterpret_cast<T*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)key * a.dvs[1];
     const float sc = a.scale;
@@ -447,7 +443,6 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         store4<T, VEC>(DV, d0, a.D, adv[t][4 * g], adv[t][4 * g + 1], adv[t][4 * g + 2], adv[t][4 * g + 3]);
       }
   }
-  wg_stamp(a.dbgbuf, a.dbg, 3);
 }
 
 // ========================================================================= backward: dQ
@@ -547,7 +542,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
     const char* ldsK = smem + (nbuf<T, DP>() == 2 ? (kt & 1) : 0) * TB;
     const char* ldsV = ldsK + I::bytes(kBK);
     const bool more = kt + 1 < nkt;
-    if (more && !(a.dbg & 1)) {
+    if (more) {
       if constexpr (VEC) {
         kst.load_buf(rk, (kt + 1) * kBK, a.ks[1], a.D, tid);
         vst.load_buf(rv, (kt + 1) * kBK, a.vs[1], a.D, tid);
@@ -556,7 +551,7 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
         vst.load(V, (kt + 1) * kBK, a.Nk, a.vs[1], a.D, tid);
       }
     }
-    const int nu = (!active || (a.dbg & 2)) ? 0 : (kt * kBK + 32 < a.Nk ? 2 : 1);   // skip padding halves / idle waves
+    const int nu = !active ? 0 : (kt * kBK + 32 < a.Nk ? 2 : 1);   // skip padding halves / idle waves
     const bool tail = (kt + 1) * kBK > a.Nk;           // only the last tile needs the key mask
 #pragma unroll 1
     for (int u = 0; u < nu; ++u) {
@@ -610,13 +605,13 @@ __global__ __launch_bounds__(256, DP >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   }
 
   if constexpr (sizeof(T) == 2 && VEC) {
-    if (active && !(a.dbg & 8)) {
+    if (active) {
       const int q0 = qb * kBQ + w * 32;
       T* DQ = reinterpret_cast<T*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
       wave_store_rows<DP>(adq, a.scale, smem + w * 32 * DP * 2, reinterpret_cast<__bf16*>(DQ), a.dqs[1],
                           a.Nq - q0, a.D, lane);
     }
-  } else if (qok && !(a.dbg & 8)) {
+  } else if (qok) {
     T* DQ = reinterpret_cast<T*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q * a.dqs[1];
     const float sc = a.scale;
 #pragma unroll

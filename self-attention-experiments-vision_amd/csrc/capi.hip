@@ -15,8 +15,8 @@
 #include "th_kernels.h"
 #include "variants.h"
 #include "fwd2.h"
-#include "fwd3.h"
 #include "bwd2.h"
+#include "bwd3.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
 #include "ln.h"
@@ -169,41 +169,35 @@ template <int DP, int NW, int MINW, bool LSUM> int fwd2_run(hipStream_t st, cons
   return check_launch("attn_fwd2");
 }
 
-// bf16 forward with two 32-row query blocks per wave (fwd3.h): NW waves x 64 query rows
-template <int DP, int NW, int MINW, bool LSUM> int fwd3_run(hipStream_t st, const AttnArgs& a) {
-  const int nqb = (a.Nq + 64 * NW - 1) / (64 * NW);
-  const long long grid = (long long)nqb * a.H * a.B;
-  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  const size_t lds = std::max(4 * (size_t)F2<DP>::TILE, (size_t)2 * NW * 32 * DP * 2);
-  if (int rc = lds_attr((const void*)attn_fwd3_kernel<DP, NW, MINW, LSUM>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd3_kernel<DP, NW, MINW, LSUM>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
-  return check_launch("attn_fwd3");
-}
-
-// SAE_FWD_VARIANT (development A/B knob): "v1" = attn_fwd_kernel; default = fwd2 4 waves, MFMA row sum
-int fwd2_variant() {
-  const char* e = getenv("SAE_FWD_VARIANT");
+// Development A/B knobs (schedule variants picked by environment variable) exist only in the
+// debug build (build.py --dev defines SAE_DEV_KNOBS); the release library takes the fixed
+// dispatch below and never reads the environment on a launch path.
+#ifdef SAE_DEV_KNOBS
+int dev_knob(const char* name) {
+  const char* e = getenv(name);
   if (!e || !*e) return 0;
   return atoi(e[0] == 'v' ? e + 1 : e);
 }
+#else
+constexpr int dev_knob(const char*) { return 0; }
+#endif
 
 template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
+#ifdef SAE_DEV_KNOBS
   switch (var) {
     case 2: return fwd2_run<DP, 8, 2, true>(st, a);
-    case 3: return fwd2_run<DP, 8, 2, false>(st, a);
     case 4: return fwd2_run<DP, 4, 2, true>(st, a);
     case 5: return fwd2_run<DP, 4, 3, true>(st, a);
     case 6: return fwd2_run<DP, 4, 3, false>(st, a);
-    case 7: if constexpr (DP <= 64) return fwd3_run<DP, 4, 2, true>(st, a); else break;
-    case 8: if constexpr (DP <= 64) return fwd3_run<DP, 8, 1, true>(st, a); else break;
-    case 9: if constexpr (DP <= 64) return fwd3_run<DP, 4, 2, false>(st, a); else break;
     default: break;
   }
-  // long key ranges at D <= 64: three waves per SIMD, row sum on the VALU (variant 6) is 2.5 %
-  // faster at N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt);
-  // at D = 128 it is 2x slower
+#endif
+  // long key ranges at D <= 64: three waves per SIMD, row sum on the VALU is 2.5 % faster at
+  // N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt); at
+  // D = 128 it is 2x slower
   if constexpr (DP <= 64)
-    if (var == 0 && a.Nk >= 512) return fwd2_run<DP, 4, 3, false>(st, a);
+    if (a.Nk >= 512) return fwd2_run<DP, 4, 3, false>(st, a);
+  (void)var;
   return fwd2_run<DP, 4, 2, true>(st, a);
 }
 
@@ -225,19 +219,39 @@ template <int DP, int NWQ, int MQ, int NWK, int MK> int bwd2_run(hipStream_t st,
   return check_launch("attn_bwd2_dkdv");
 }
 
-int bwd2_variant() {
-  const char* e = getenv("SAE_BWD_VARIANT");
-  if (!e || !*e) return 0;
-  return atoi(e[0] == 'v' ? e + 1 : e);
+template <int DP> int bwd2_run_default(hipStream_t st, const AttnArgs& a) {
+  return bwd2_run<DP, 4, 2, 4, 2>(st, a);
 }
 
-template <int DP> int bwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
-  switch (var) {
-    case 3: return bwd2_run<DP, 4, 3, 4, 2>(st, a);
-    case 4: return bwd2_run<DP, 8, 2, 8, 2>(st, a);
-    case 5: return bwd2_run<DP, 4, 2, 8, 2>(st, a);
-    default: return bwd2_run<DP, 4, 2, 4, 2>(st, a);
+// single-pass bf16 backward (bwd3.h): 256 keys per workgroup (4 waves x 2 sub-blocks of 32 keys);
+// with more than one key block per (batch, head) the fp32 dQ partials are summed by
+// attn_bwd3_dq_reduce
+constexpr int kB3Keys = 256;
+
+size_t bwd3_partial_bytes(const sae_attn_desc* d) {
+  const int dp = pick_dp(d->head_dim);
+  if (d->dtype != SAE_DTYPE_BF16 || dp > 64) return 0;
+  const long long nkb = (d->seq_k + kB3Keys - 1) / kB3Keys;
+  if (nkb <= 1) return 0;
+  return (size_t)nkb * d->batch * d->heads * d->seq_q * dp * sizeof(float);
+}
+
+template <int DP, int NW, int KPW> int bwd3_run(hipStream_t st, const AttnArgs& a) {
+  using C = B3<DP, NW, KPW>;
+  static_assert(C::BK == kB3Keys, "workspace sizing assumes 256-key blocks");
+  const int nkb = (a.Nk + C::BK - 1) / C::BK;
+  const long long grid = (long long)nkb * a.H * a.B;
+  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  if (nkb > 1 && !a.dqp) return fail(SAE_EINVAL, "bwd3: workspace too small for the dQ partials");
+  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW>, C::LDS)) return rc;
+  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
+  if (int rc = check_launch("attn_bwd3")) return rc;
+  if (nkb > 1) {
+    const long long n = (long long)a.B * a.H * a.Nq * (DP / 8);
+    hipLaunchKernelGGL(attn_bwd3_dq_reduce_kernel<DP>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, nkb);
+    return check_launch("attn_bwd3_dq_reduce");
   }
+  return SAE_OK;
 }
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
@@ -428,9 +442,7 @@ int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void
   const bool vec = d->head_dim % epc == 0 && strides_vec(d->q_stride, epc) && strides_vec(d->k_stride, epc) &&
                    strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o);
-  const int var = fwd2_variant();
-  if (const char* e = getenv("SAE_DBG")) a.dbg = atoi(e);
-  if (const char* e = getenv("SAE_DBG_BUF")) a.dbgbuf = (unsigned long long*)strtoull(e, nullptr, 16);
+  const int var = dev_knob("SAE_FWD_VARIANT");
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     if (dp == 32) return fwd2_dispatch<32>((hipStream_t)stream, a, var);
@@ -440,9 +452,13 @@ int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void
   return dispatch<FwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }
 
+static size_t delta_bytes(const sae_attn_desc* d) {
+  return (((size_t)d->batch * d->heads * d->seq_q * sizeof(float)) + 255) & ~(size_t)255;
+}
+
 size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
   if (!d) return 0;
-  return (((size_t)d->batch * d->heads * d->seq_q * sizeof(float)) + 255) & ~(size_t)255;
+  return delta_bytes(d) + bwd3_partial_bytes(d);
 }
 
 int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
@@ -457,8 +473,6 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
     return fail(SAE_EINVAL, "SAE_FLAG_RELPOS needs bias_h, bias_w, dbias_h, dbias_w");
   AttnArgs a;
   fill_args(a, d);
-  if (const char* e = getenv("SAE_DBG")) a.dbg = atoi(e);
-  if (const char* e = getenv("SAE_DBG_BUF")) a.dbgbuf = (unsigned long long*)strtoull(e, nullptr, 16);
   a.q = q;
   a.k = k;
   a.v = v;
@@ -469,6 +483,7 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
   a.dk = dk;
   a.dv = dv;
   a.delta = reinterpret_cast<float*>(workspace);
+  if (bwd3_partial_bytes(d)) a.dqp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + delta_bytes(d));
   a.bias_h = bias_h;
   a.bias_w = bias_w;
   a.dbias_h = dbias_h;
@@ -480,12 +495,23 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
                    strides_vec(d->dk_stride, epc) && strides_vec(d->dv_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o) && aligned16(dout) && aligned16(dq) &&
                    aligned16(dk) && aligned16(dv);
-  const int var = bwd2_variant();
+  const int var = dev_knob("SAE_BWD_VARIANT");
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
-    // head_dim 128 (BoTNet) stays on the v1 kernels: bwd2 at DP = 128 runs out of registers
-    if (dp == 32) return bwd2_dispatch<32>((hipStream_t)stream, a, var);
-    if (dp == 64) return bwd2_dispatch<64>((hipStream_t)stream, a, var);
+    hipStream_t st = (hipStream_t)stream;
+    // head_dim 128 (BoTNet) stays on the v1 kernels (register budget of the lean passes)
+    if (var == 2) {   // two-pass bwd2 (development A/B only: var is 0 in the release build)
+      if (dp == 32) return bwd2_run_default<32>(st, a);
+      if (dp == 64) return bwd2_run_default<64>(st, a);
+    }
+#ifdef SAE_DEV_KNOBS
+    if (var == 3) {   // eight waves x one 32-key sub-block (two waves per SIMD)
+      if (dp == 32) return bwd3_run<32, 8, 1>(st, a);
+      if (dp == 64) return bwd3_run<64, 8, 1>(st, a);
+    }
+#endif
+    if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
+    if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
   }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }

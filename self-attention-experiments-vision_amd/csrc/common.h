@@ -282,19 +282,6 @@ __device__ __forceinline__ void wave_store_rows(const f32x16* acc, float sc, cha
   __builtin_amdgcn_wave_barrier();
 }
 
-// ------------------------------------------------------------------ diagnostic timestamps
-// Per-workgroup timeline (SAE_DBG & 64 only; never in a production launch): slot k of the
-// workgroup's 8-word record gets s_memrealtime (100 MHz); words 6/7 hold HW_ID and XCC_ID.
-__device__ __forceinline__ void wg_stamp(unsigned long long* buf, int dbg, int slot) {
-  if (!(dbg & 64) || threadIdx.x != 0) return;
-  unsigned long long t = __builtin_amdgcn_s_memrealtime();
-  buf[blockIdx.x * 8 + slot] = t;
-  if (slot == 0) {
-    buf[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    buf[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-  }
-}
-
 // XCD-aware block order (cdna_hip_programming.md T1, bijective form): hardware block `bid` of a
 // G-block grid runs on XCD bid % 8; returning logical ids so that consecutive logical blocks
 // (which share K/V or Q/dO of one (batch, head)) land on the same XCD and its L2.

@@ -199,8 +199,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
 
-  wg_stamp(a.dbgbuf, a.dbg, 0);
-  if (a.dbg & 4) return;
   // K/V tiles staged global -> registers -> LDS: tile t + 1 is loaded while tile t computes
   // (a second register stage in flight measured no faster and costs the third wave per SIMD)
   F2Stage<DP, NW> kst, vst;
@@ -248,7 +246,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   vst.write(smem + TILE);
   vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
   __syncthreads();
-  wg_stamp(a.dbgbuf, a.dbg, 1);
   // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1 into the other
   // buffer, barrier.  Buffer selection and the peeled first tile are compile-time, so the
   // first tile's zero accumulators become the MFMA's C operand and its rescale disappears.
@@ -282,8 +279,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   if (active) sweep(std::true_type{});
   else sweep(std::false_type{});
 
-  wg_stamp(a.dbgbuf, a.dbg, 2);
-  if (!active || (a.dbg & 8)) return;
+  if (!active) return;
   float lt;
   if constexpr (LSUM) lt = lacc[0];
   else lt = xhalf_sum(l);
@@ -298,7 +294,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
     wave_store_rows<DP>(acco, 1.f, smem + w * 32 * DP * 2, O, a.os[1], a.Nq - q0, a.D, lane);
   }
   if (q < a.Nq && h == 0 && a.lse) a.lse[((size_t)b * a.H + hh) * a.Nq + q] = (m + lg2(lt)) * kLn2;
-  wg_stamp(a.dbgbuf, a.dbg, 3);
 }
 
 }  // namespace sae

@@ -599,8 +599,18 @@ def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = N
         raise ValueError(f"gemm_nt: a2 {tuple(a2.shape)} and bt {tuple(bt.shape)} disagree on K")
     if bt.stride(1) != 1:
         bt = bt.contiguous()
-    c = out if out is not None else torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
-    c2 = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device) if epilogue == EPI_GELU else None
+    if out is not None:
+        if out.dtype != torch.bfloat16 or out.dim() != 2 or tuple(out.shape) != (M, N) or out.stride(1) != 1:
+            raise ValueError(f"gemm_nt: out must be bf16 [{M}, {N}] with unit column stride")
+        c = out
+    else:
+        c = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
+    # the kernel writes c2 with c's row stride (ldc): give it the same layout
+    c2 = torch.empty_strided((M, N), (c.stride(0), 1), dtype=torch.bfloat16, device=a2.device) \
+        if epilogue == EPI_GELU else None
+    if epilogue == EPI_DGELU:
+        if aux is None or aux.dtype != torch.bfloat16 or tuple(aux.shape) != (M, N):
+            raise ValueError(f"gemm_nt: the GELU-derivative epilogue needs a bf16 aux [{M}, {N}]")
     if aux is not None and aux.stride(1) != 1:
         aux = aux.contiguous()
     if bias is not None:
@@ -677,8 +687,25 @@ def layer_norm_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.float32 and C % 4 == 0 and C <= 1024 and x.is_contiguous()
 
 
+def _f32c(t: torch.Tensor, what: str) -> torch.Tensor:
+    """fp32 contiguous view/copy of a LayerNorm operand (the kernels read raw fp32)."""
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _bf16c(t: torch.Tensor) -> torch.Tensor:
+    """bf16 contiguous copy of a LayerNorm operand (the kernels read raw bf16)."""
+    if t.dtype != torch.bfloat16:
+        t = t.to(torch.bfloat16)
+    return t if t.is_contiguous() else t.contiguous()
+
+
 def _ln_fwd(x, delta, gamma, beta, eps):
     lib = L.load()
+    x, gamma, beta = _f32c(x, "x"), _f32c(gamma, "gamma"), _f32c(beta, "beta")
+    if delta is not None:
+        delta = _bf16c(delta)
     C = x.shape[-1]
     M = x.numel() // C
     y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
@@ -694,14 +721,15 @@ def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta):
     lib = L.load()
     C = xs.shape[-1]
     M = xs.numel() // C
-    dy = dy.contiguous()
+    xs, gamma = _f32c(xs, "x"), _f32c(gamma, "gamma")
+    dy = _bf16c(dy)
     dx = torch.empty_like(xs)
     ddelta = torch.empty(xs.shape, dtype=torch.bfloat16, device=xs.device) if want_ddelta else None
     dg = torch.empty(C, dtype=torch.float32, device=xs.device)
     db = torch.empty(C, dtype=torch.float32, device=xs.device)
     ws = torch.empty(lib.sae_layernorm_bwd_workspace_bytes(M, C), dtype=torch.uint8, device=xs.device)
     if dxin is not None:
-        dxin = dxin.contiguous()
+        dxin = _f32c(dxin, "dxin")
     L.check(lib.sae_layernorm_bwd(_stream(xs), M, C, _ptr(xs), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dy),
                                   _ptr(dxin), _ptr(dx), _ptr(ddelta), _ptr(dg), _ptr(db), _ptr(ws)))
     return dx, ddelta, dg, db
@@ -724,7 +752,7 @@ class _LayerNorm(torch.autograd.Function):
 class _AddLayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, delta, gamma, beta, eps):
-        xout, y, mean, rstd = _ln_fwd(x, delta.contiguous(), gamma, beta, eps)
+        xout, y, mean, rstd = _ln_fwd(x, delta, gamma, beta, eps)
         ctx.save_for_backward(xout, mean, rstd, gamma)
         ctx.delta_dtype = delta.dtype
         return xout, y
@@ -746,7 +774,9 @@ class _AddLayerNormScaled(torch.autograd.Function):
         lib = L.load()
         C = x.shape[-1]
         M = x.numel() // C
-        delta = delta.contiguous()
+        x, gamma, beta = _f32c(x, "x"), _f32c(gamma, "gamma"), _f32c(beta, "beta")
+        delta_dtype = delta.dtype
+        delta = _bf16c(delta)
         # the reference casts the LayerScale parameter to the compute dtype (layerscale.py:22)
         lsf = ls.detach().to(delta.dtype).float().contiguous()
         y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
@@ -757,7 +787,7 @@ class _AddLayerNormScaled(torch.autograd.Function):
                                              _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), float(eps), _ptr(lsf),
                                              _ptr(rowscale), int(rpb)))
         ctx.save_for_backward(xout, mean, rstd, gamma, delta, lsf, rowscale)
-        ctx.rpb, ctx.delta_dtype, ctx.ls_dtype = int(rpb), delta.dtype, ls.dtype
+        ctx.rpb, ctx.delta_dtype, ctx.ls_dtype = int(rpb), delta_dtype, ls.dtype
         return xout, y
 
     @staticmethod
@@ -768,8 +798,9 @@ class _AddLayerNormScaled(torch.autograd.Function):
         M = xout.numel() // C
         if dy is None:
             dy = torch.zeros(xout.shape, dtype=torch.bfloat16, device=xout.device)
-        dy = dy.contiguous()
-        dxin = dxout.contiguous() if dxout is not None else None
+        dy = _bf16c(dy)
+        gamma = _f32c(gamma, "gamma")
+        dxin = _f32c(dxout, "dxin") if dxout is not None else None
         dx = torch.empty_like(xout)
         ddelta = torch.empty(xout.shape, dtype=torch.bfloat16, device=xout.device)
         dg = torch.empty(C, dtype=torch.float32, device=xout.device)

@@ -90,12 +90,35 @@ class TrainStep:
     def _capture(self, images: torch.Tensor, labels: torch.Tensor):
         self._images = images.clone()
         self._labels = labels.clone()
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        snap = [p.detach().clone() for p in params]
+        had_state = {id(p) for p in params if p in self.opt.state and self.opt.state[p]}
+        snap_state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
+                      for p in params if id(p) in had_state}
         s = torch.cuda.Stream(device=images.device)
         s.wait_stream(torch.cuda.current_stream(images.device))
         with torch.cuda.stream(s):   # warm-up on a side stream (allocator / library state)
             for _ in range(2):
                 self._eager(self._images, self._labels)
         torch.cuda.current_stream(images.device).wait_stream(s)
+        # the warm-up steps were only for the allocator and the optimizer's lazily created state:
+        # put parameters and optimizer state back, so that the first call performs exactly ONE
+        # update (the reference's one update per batch, train.py:94-100)
+        with torch.no_grad():
+            for p, v in zip(params, snap):
+                p.copy_(v)
+            for p in params:
+                st = self.opt.state.get(p)
+                if not st:
+                    continue
+                old = snap_state.get(id(p))
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if old is not None and torch.is_tensor(old.get(k)):
+                        v.copy_(old[k])
+                    else:   # state created by the warm-up: a fresh optimizer's zeros
+                        v.zero_()
         g = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         try:

@@ -96,8 +96,29 @@ def test_gemm_nt_rejects(dev):
         ops.gemm_nt(a, bt)
     a = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
     bt = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
-    with pytest.raises(SaeError):                                   # DGELU without aux
+    with pytest.raises((SaeError, ValueError)):                     # DGELU without aux
         ops.gemm_nt(a, bt, None, ops.EPI_DGELU)
+    with pytest.raises(ValueError):                                 # out of the wrong dtype
+        ops.gemm_nt(a, bt, out=torch.empty(64, 64, device=dev))
+
+
+def test_gemm_nt_strided_out_gelu(dev):
+    """A caller-provided out with a row stride larger than N, GELU epilogue: c and the
+    pre-activation c2 (allocated with out's row stride) both hold the right values."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(4)
+    M, N, K = 200, 96, 128
+    a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    bt = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+    big = torch.full((M, 160), 7.0, device=dev, dtype=torch.bfloat16)
+    out = big[:, 16:16 + N]
+    c, h = ops.gemm_nt(a, bt, None, ops.EPI_GELU, out=out)
+    ref = (a.float() @ bt.float().t()).to(torch.bfloat16)
+    assert c.data_ptr() == out.data_ptr() and h.stride(0) == out.stride(0)
+    assert float((h.float() - ref.float()).abs().max()) <= 2e-2 * float(ref.float().abs().max())
+    gl = torch.nn.functional.gelu(h.float(), approximate="tanh")
+    assert float((c.float() - gl).abs().max()) <= 2e-2 * float(gl.abs().max())
+    assert torch.all(big[:, :16] == 7.0) and torch.all(big[:, 16 + N:] == 7.0)
 
 
 def test_weight_cast_exact(dev):

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--shapes", default="deit_s,vitb384,cait_s24,cait_ca,bot14,bot7")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
-    ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B")
+    ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B (dev build: SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so)")
     ap.add_argument("--bwd-variants", default="", help="comma list of SAE_BWD_VARIANT values to A/B")
     args = ap.parse_args()
     import torch
