@@ -36,7 +36,6 @@ struct AttnArgs {
   void* dk;
   void* dv;
   float* delta;     // bwd workspace [B, H, Nq]
-  float* dqp;       // bwd3 workspace: per-key-block dQ partials [nkb][B, H, Nq, DP] (fp32)
   const float* bias_h;
   const float* bias_w;
   float* dbias_h;

@@ -13,10 +13,13 @@
 //     split over the waves as 16 x 16 output tiles (v_mfma_f32_16x16x32_bf16), each summing over
 //     all keys of the block, the K^T operand fragments held in registers for the whole sweep;
 //   * delta = rowsum(dO o O) is formed while the dO / O tile is staged (no separate pass).
-// Five products per tile instead of seven.  Key blocks: 32 * NW keys; when Nk needs more than one
-// block the per-block dQ partials (fp32) go to the workspace and attn_bwd3_dq_reduce sums them in
-// block order (deterministic: no atomics anywhere).  Software pipeline: tile t's dQ runs in
-// iteration t + 1 from the other dS image, so each query tile costs ONE workgroup barrier.
+// Five products per tile instead of seven, and dQ needs no sum across workgroups: the kernel takes
+// key ranges of up to 32 * NW * KPW = 256 keys (every N <= 256 config: DeiT / ViT at 224 px, CaiT,
+// BoTNet, CeiT, TNT), one workgroup per (batch, head).  Longer key ranges stay on bwd2.h: split
+// over several workgroups, the fp32 dQ partials plus their ordered sum cost more than the two-pass
+// recompute (ViT-B/16@384: 441 vs 335 us, profiles/r02_bwd3_ab.txt).  Software pipeline: tile t's
+// dQ runs in iteration t + 1 from the other dS image, so each query tile costs ONE barrier.
+// Deterministic: no atomics.
 #pragma once
 #include "fwd2.h"
 
@@ -123,15 +126,12 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const dsb = smem + 2 * TB;   // two dS^T images (the K image during the prologue)
 
-  const int nkb = (a.Nk + BK - 1) / BK;
-  int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int kb = bid % nkb;
-  bid /= nkb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int hh = bid % a.H;
   const int b = bid / a.H;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int key0 = kb * BK;
+  constexpr int key0 = 0;                     // the whole key range is this workgroup's (Nk <= BK)
   const int wrow = w * 32 * KPW;              // first key (image row) of this wave
   const bool active = key0 + wrow < a.Nk;     // wave-uniform: this wave holds at least one key
   const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
@@ -269,16 +269,11 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       const int qq = qt * 32 + 16 * qhs[t] + li;
       const int d0 = 16 * db + 4 * gq;
       if (qq < a.Nq && d0 < a.D) {
-        if (nkb == 1) {
-          typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-          const bf16x4 v = {(__bf16)(acc[0] * a.scale), (__bf16)(acc[1] * a.scale), (__bf16)(acc[2] * a.scale),
-                            (__bf16)(acc[3] * a.scale)};
-          __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)qq * a.dqs[1];
-          *reinterpret_cast<bf16x4*>(DQ + d0) = v;
-        } else {
-          float* P = a.dqp + (((size_t)kb * a.B * a.H + (size_t)b * a.H + hh) * a.Nq + qq) * DP + d0;
-          *reinterpret_cast<f32x4*>(P) = acc;
-        }
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        const bf16x4 v = {(__bf16)(acc[0] * a.scale), (__bf16)(acc[1] * a.scale), (__bf16)(acc[2] * a.scale),
+                          (__bf16)(acc[3] * a.scale)};
+        __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)qq * a.dqs[1];
+        *reinterpret_cast<bf16x4*>(DQ + d0) = v;
       }
     }
   };
@@ -392,37 +387,6 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       wave_store_rows<DP>(adv[j], 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
     }
   }
-}
-
-// dQ = scale * sum over key blocks of the fp32 partials, in block order (deterministic).
-// One thread per 8 head-dim elements of one query row.
-template <int DP>
-__global__ __launch_bounds__(256) void attn_bwd3_dq_reduce_kernel(AttnArgs a, int nkb) {
-  constexpr int CPR = DP / 8;
-  const long long total = (long long)a.B * a.H * a.Nq * CPR;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int c = (int)(i % CPR);
-  long long t = i / CPR;
-  const int q = (int)(t % a.Nq);
-  t /= a.Nq;                         // t = b * H + hh
-  if (c * 8 >= a.D) return;
-  const size_t plane = (size_t)a.B * a.H * a.Nq * DP;
-  const float* p = a.dqp + ((size_t)t * a.Nq + q) * DP + c * 8;
-  f32x4 s0 = *reinterpret_cast<const f32x4*>(p), s1 = *reinterpret_cast<const f32x4*>(p + 4);
-  for (int kb = 1; kb < nkb; ++kb) {
-    s0 += *reinterpret_cast<const f32x4*>(p + kb * plane);
-    s1 += *reinterpret_cast<const f32x4*>(p + kb * plane + 4);
-  }
-  const int hh = (int)(t % a.H), b = (int)(t / a.H);
-  bf16x8 v;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = (__bf16)(s0[j] * a.scale);
-    v[4 + j] = (__bf16)(s1[j] * a.scale);
-  }
-  __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q * a.dqs[1];
-  *reinterpret_cast<bf16x8*>(DQ + c * 8) = v;
 }
 
 }  // namespace sae

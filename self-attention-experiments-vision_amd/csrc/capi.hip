@@ -223,35 +223,19 @@ template <int DP> int bwd2_run_default(hipStream_t st, const AttnArgs& a) {
   return bwd2_run<DP, 4, 2, 4, 2>(st, a);
 }
 
-// single-pass bf16 backward (bwd3.h): 256 keys per workgroup (4 waves x 2 sub-blocks of 32 keys);
-// with more than one key block per (batch, head) the fp32 dQ partials are summed by
-// attn_bwd3_dq_reduce
+// single-pass bf16 backward (bwd3.h): one workgroup per (batch, head) holding all Nk <= 256 keys
+// (8 waves x 32 keys, two waves per SIMD); longer key ranges take the two-pass bwd2
 constexpr int kB3Keys = 256;
-
-size_t bwd3_partial_bytes(const sae_attn_desc* d) {
-  const int dp = pick_dp(d->head_dim);
-  if (d->dtype != SAE_DTYPE_BF16 || dp > 64) return 0;
-  const long long nkb = (d->seq_k + kB3Keys - 1) / kB3Keys;
-  if (nkb <= 1) return 0;
-  return (size_t)nkb * d->batch * d->heads * d->seq_q * dp * sizeof(float);
-}
 
 template <int DP, int NW, int KPW> int bwd3_run(hipStream_t st, const AttnArgs& a) {
   using C = B3<DP, NW, KPW>;
-  static_assert(C::BK == kB3Keys, "workspace sizing assumes 256-key blocks");
-  const int nkb = (a.Nk + C::BK - 1) / C::BK;
-  const long long grid = (long long)nkb * a.H * a.B;
+  static_assert(C::BK == kB3Keys, "bwd3 dispatch assumes 256-key blocks");
+  const long long grid = (long long)a.H * a.B;
+  if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3: %d keys > %d", a.Nk, C::BK);
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  if (nkb > 1 && !a.dqp) return fail(SAE_EINVAL, "bwd3: workspace too small for the dQ partials");
   if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW>, C::LDS)) return rc;
   hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
-  if (int rc = check_launch("attn_bwd3")) return rc;
-  if (nkb > 1) {
-    const long long n = (long long)a.B * a.H * a.Nq * (DP / 8);
-    hipLaunchKernelGGL(attn_bwd3_dq_reduce_kernel<DP>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, nkb);
-    return check_launch("attn_bwd3_dq_reduce");
-  }
-  return SAE_OK;
+  return check_launch("attn_bwd3");
 }
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
@@ -458,7 +442,7 @@ static size_t delta_bytes(const sae_attn_desc* d) {
 
 size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
   if (!d) return 0;
-  return delta_bytes(d) + bwd3_partial_bytes(d);
+  return delta_bytes(d);
 }
 
 int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
@@ -483,7 +467,6 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
   a.dk = dk;
   a.dv = dv;
   a.delta = reinterpret_cast<float*>(workspace);
-  if (bwd3_partial_bytes(d)) a.dqp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + delta_bytes(d));
   a.bias_h = bias_h;
   a.bias_w = bias_w;
   a.dbias_h = dbias_h;
@@ -500,18 +483,18 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;
     // head_dim 128 (BoTNet) stays on the v1 kernels (register budget of the lean passes)
-    if (var == 2) {   // two-pass bwd2 (development A/B only: var is 0 in the release build)
-      if (dp == 32) return bwd2_run_default<32>(st, a);
-      if (dp == 64) return bwd2_run_default<64>(st, a);
-    }
+    if (a.Nk <= kB3Keys && var != 2) {
 #ifdef SAE_DEV_KNOBS
-    if (var == 3) {   // eight waves x one 32-key sub-block (two waves per SIMD)
+      if (var == 3) {   // four waves x two 32-key sub-blocks (one wave per SIMD): measured slower
+        if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
+        if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
+      }
+#endif
       if (dp == 32) return bwd3_run<32, 8, 1>(st, a);
       if (dp == 64) return bwd3_run<64, 8, 1>(st, a);
     }
-#endif
-    if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
-    if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
+    if (dp == 32) return bwd2_run_default<32>(st, a);
+    if (dp == 64) return bwd2_run_default<64>(st, a);
   }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }
