@@ -43,7 +43,7 @@ __all__ = [
     "to_absolute_logits", "relative_logits_1d", "relative_logits",
     "relative_logits_indexed", "relpos_bias_tables", "attention_core_fwd",
     "attention_core_bwd", "AttnParams", "attention_block_fwd",
-    "attention_block_bwd", "class_query", "lc_query", "logsumexp",
+    "attention_block_bwd", "attention_block_bwd_bf16", "class_query", "lc_query", "logsumexp",
 ]
 
 
@@ -391,6 +391,48 @@ def attention_block_bwd(x_q, x_kv, p: AttnParams, dy, rotary: bool = False):
         g["values_bias"] = dv.sum(axis=(0, 1))
     g["x_q"] = np.einsum("bnhd,chd->bnc", dq, Wq)
     g["x_kv"] = np.einsum("bnhd,chd->bnc", dk, Wk) + np.einsum("bnhd,chd->bnc", dv, Wv)
+    g["dq"], g["dk"], g["dv"], g["do"] = dq, dk, dv, do
+    return g
+
+
+def _rb(x):
+    """bf16 rounding, kept in float64 (the accumulation type of the emulated dot products)."""
+    return round_bf16(np.asarray(x, np.float32)).astype(np.float64)
+
+
+def attention_block_bwd_bf16(x_q, x_kv, p: AttnParams, dy):
+    """bf16-emulated JAX autodiff of ``attention_block_fwd(..., "bf16")`` (no talking heads,
+    no rotary): the cotangent of every bf16 value is bf16 (each dot_general / elementwise op of
+    the backward rounds its output; products accumulate in wider precision), the gradient of a
+    bf16-cast fp32 parameter is the bf16 cotangent cast back to fp32.  jax.nn.softmax's VJP
+    (jax 0.2.x) is ``p * (g - sum(g * p))`` evaluated in bf16.  Returns the same keys as
+    :func:`attention_block_bwd`."""
+    if p.th1 is not None or p.th2 is not None:
+        raise NotImplementedError("bf16 chain: talking heads run their mix in fp32 (survey D8)")
+    y, aux = attention_block_fwd(x_q, x_kv, p, "bf16", return_aux=True)
+    f = lambda t: np.asarray(t, np.float64)
+    xq, xkv = _rb(x_q), _rb(x_kv)
+    Wq, Wk, Wv, Wo = (_rb(t) for t in (p.queries, p.keys, p.values, p.out))
+    q, k, v, o = (f(aux[n]) for n in ("q", "k", "v", "o"))
+    qh, pr = f(aux["qhat"]), f(aux["p"])
+    D = q.shape[-1]
+    g = {}
+    dyb = _rb(dy)
+    g["DenseGeneral_0"] = _rb(np.einsum("bnhd,bnc->hdc", o, dyb))
+    do = _rb(np.einsum("bnc,hdc->bnhd", dyb, Wo))
+    dv = _rb(np.einsum("bhqk,bqhd->bkhd", pr, do))
+    dp = _rb(np.einsum("bqhd,bkhd->bhqk", do, v))
+    t = _rb(dp * pr)
+    sm = _rb(t.sum(-1, keepdims=True))
+    ds = _rb(pr * _rb(dp - sm))
+    dqh = _rb(np.einsum("bhqk,bkhd->bqhd", ds, k))
+    dk = _rb(np.einsum("bhqk,bqhd->bkhd", ds, qh))
+    dq = _rb(dqh / np.sqrt(D))
+    g["queries"] = _rb(np.einsum("bnc,bnhd->chd", xq, dq))
+    g["keys"] = _rb(np.einsum("bnc,bnhd->chd", xkv, dk))
+    g["values"] = _rb(np.einsum("bnc,bnhd->chd", xkv, dv))
+    g["x_q"] = _rb(np.einsum("bnhd,chd->bnc", dq, Wq))
+    g["x_kv"] = _rb(_rb(np.einsum("bnhd,chd->bnc", dk, Wk)) + _rb(np.einsum("bnhd,chd->bnc", dv, Wv)))
     g["dq"], g["dk"], g["dv"], g["do"] = dq, dk, dv, do
     return g
 

@@ -185,3 +185,112 @@ def adam_update(params, grads, state, lr=5e-4, b1=0.9, b2=0.999, eps=1e-8, wd=1e
         mh = m / (1 - b1 ** t)
         vh = v / (1 - b2 ** t)
         params[k] -= lr * (mh / (np.sqrt(vh) + eps) + wd * params[k])
+
+
+# ------------------------------------------------------------------ bf16-emulated training step
+def _rb(x):
+    """Round to bfloat16 (ties to even), kept in float64: the emulated dot products accumulate wide
+    and round their outputs, as XLA does for bf16 dot_general."""
+    a = np.ascontiguousarray(np.asarray(x, np.float32))
+    u = a.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def _softmax_bf16(s):
+    m = s.max(-1, keepdims=True)
+    e = _rb(np.exp(_rb(s - m)))
+    return _rb(e / _rb(e.sum(-1, keepdims=True)))
+
+
+def vit_loss_and_grads_bf16(params: Dict[str, np.ndarray], images, labels, num_layers: int, num_heads: int,
+                            patch: int, smoothing: float = 0.1):
+    """The training step of ``create_model(..., dtype=jnp.bfloat16)`` (train.py:222-224) with the
+    reference's bf16 rounding points: every Dense / DenseGeneral casts input and kernel to bf16 and
+    returns bf16 (bias cast to bf16 and added in bf16), LayerNorm computes in fp32 and returns bf16,
+    the attention internals are bf16 (attention.py:29-63), GELU returns bf16, the residual stream is
+    fp32 (promoted by the fp32 cls / pos-embed params, vit.py:46,85).  Backward is JAX autodiff of
+    that program: the cotangent of every bf16 value is bf16, a bf16-cast fp32 parameter receives its
+    bf16 cotangent cast to fp32.  Returns (loss, logits, grads) like :func:`vit_loss_and_grads`."""
+    P = {k: np.asarray(v, np.float64) for k, v in params.items()}
+    r = _rb
+    B = images.shape[0]
+    pe_in = r(patchify(np.asarray(images, np.float64), patch))
+    Wp = r(P["PatchEmbedBlock_0.Dense_0.kernel"])
+    pe = r(pe_in @ Wp)
+    C = pe.shape[-1]
+    x = np.concatenate([np.broadcast_to(P["cls"], (B, 1, C)), pe], 1) + P["Encoder_0.AddAbsPosEmbed_0.pos_embed"]
+    caches = []
+    for i in range(num_layers):
+        pre = f"Encoder_0.EncoderBlock_{i}."
+        h1f, c1 = layer_norm(x, P[pre + "LayerNorm_0.scale"], P[pre + "LayerNorm_0.bias"])
+        h1 = r(h1f)
+        W = [r(P[pre + f"SelfAttentionBlock_0.{n}.kernel"]) for n in ("queries", "keys", "values", "DenseGeneral_0")]
+        Hh, D = W[0].shape[1], W[0].shape[2]
+        N = h1.shape[1]
+        q, k, v = (r(h1 @ w.reshape(C, Hh * D)).reshape(B, N, Hh, D).transpose(0, 2, 1, 3) for w in W[:3])
+        qh = r(q / np.sqrt(D))
+        p = _softmax_bf16(r(qh @ k.transpose(0, 1, 3, 2)))
+        o = r(p @ v).transpose(0, 2, 1, 3).reshape(B, N, Hh * D)
+        a = r(o @ W[3].reshape(Hh * D, C))
+        x = x + a
+        h2f, c2 = layer_norm(x, P[pre + "LayerNorm_1.scale"], P[pre + "LayerNorm_1.bias"])
+        h2 = r(h2f)
+        W1, W2 = r(P[pre + "FFBlock_0.Dense_0.kernel"]), r(P[pre + "FFBlock_0.Dense_1.kernel"])
+        u = r(r(h2 @ W1) + r(P[pre + "FFBlock_0.Dense_0.bias"]))
+        g = r(gelu_tanh(u))
+        f = r(r(g @ W2) + r(P[pre + "FFBlock_0.Dense_1.bias"]))
+        x = x + f
+        caches.append((c1, h1, W, q, k, v, qh, p, o, c2, h2, W1, W2, u, g))
+    zf, cz = layer_norm(x, P["Encoder_0.LayerNorm_0.scale"], P["Encoder_0.LayerNorm_0.bias"])
+    z = r(zf)
+    Wd = r(P["Dense_0.kernel"])
+    logits = r(r(z[:, 0] @ Wd) + r(P["Dense_0.bias"]))
+    loss, dlogits = smoothed_ce(logits, labels, smoothing, logits.shape[-1])
+
+    G = {}
+    dl = r(dlogits)
+    G["Dense_0.kernel"] = r(z[:, 0].T @ dl)
+    G["Dense_0.bias"] = r(dl.sum(0))
+    dz = np.zeros_like(z)
+    dz[:, 0] = r(dl @ Wd.T)
+    dx, G["Encoder_0.LayerNorm_0.scale"], G["Encoder_0.LayerNorm_0.bias"] = layer_norm_bwd(
+        dz, P["Encoder_0.LayerNorm_0.scale"], cz)
+    for i in reversed(range(num_layers)):
+        pre = f"Encoder_0.EncoderBlock_{i}."
+        c1, h1, W, q, k, v, qh, p, o, c2, h2, W1, W2, u, g = caches[i]
+        Hh, D = W[0].shape[1], W[0].shape[2]
+        N = h1.shape[1]
+        df = r(dx)
+        G[pre + "FFBlock_0.Dense_1.kernel"] = r(g.reshape(-1, g.shape[-1]).T @ df.reshape(-1, C))
+        G[pre + "FFBlock_0.Dense_1.bias"] = r(df.reshape(-1, C).sum(0))
+        dg = r(df @ W2.T)
+        du = r(dg * gelu_tanh_grad(u))
+        G[pre + "FFBlock_0.Dense_0.kernel"] = r(h2.reshape(-1, C).T @ du.reshape(-1, du.shape[-1]))
+        G[pre + "FFBlock_0.Dense_0.bias"] = r(du.reshape(-1, du.shape[-1]).sum(0))
+        dh2 = r(du @ W1.T)
+        dxx, G[pre + "LayerNorm_1.scale"], G[pre + "LayerNorm_1.bias"] = layer_norm_bwd(
+            dh2, P[pre + "LayerNorm_1.scale"], c2)
+        dx = dx + dxx
+        da = r(dx)
+        G[pre + "SelfAttentionBlock_0.DenseGeneral_0.kernel"] = r(o.reshape(-1, Hh * D).T @ da.reshape(-1, C)).reshape(Hh, D, C)
+        do = r(da @ W[3].reshape(Hh * D, C).T).reshape(B, N, Hh, D).transpose(0, 2, 1, 3)
+        dv = r(p.transpose(0, 1, 3, 2) @ do)
+        dp = r(do @ v.transpose(0, 1, 3, 2))
+        ds = r(p * r(dp - r(r(dp * p).sum(-1, keepdims=True))))
+        dq = r(r(ds @ k) / np.sqrt(D))
+        dk = r(ds.transpose(0, 1, 3, 2) @ qh)
+        tok = lambda t: t.transpose(0, 2, 1, 3).reshape(B * N, Hh * D)
+        h1_2 = h1.reshape(B * N, C)
+        for n, dd in (("queries", dq), ("keys", dk), ("values", dv)):
+            G[pre + f"SelfAttentionBlock_0.{n}.kernel"] = r(h1_2.T @ tok(dd)).reshape(C, Hh, D)
+        dh1 = r(r(r(tok(dq) @ W[0].reshape(C, Hh * D).T) + r(tok(dk) @ W[1].reshape(C, Hh * D).T))
+                + r(tok(dv) @ W[2].reshape(C, Hh * D).T)).reshape(B, N, C)
+        dxx, G[pre + "LayerNorm_0.scale"], G[pre + "LayerNorm_0.bias"] = layer_norm_bwd(
+            dh1, P[pre + "LayerNorm_0.scale"], c1)
+        dx = dx + dxx
+    G["Encoder_0.AddAbsPosEmbed_0.pos_embed"] = dx.sum(0, keepdims=True)
+    G["cls"] = dx[:, 0:1].sum(0, keepdims=True)
+    dpe = r(dx[:, 1:])
+    G["PatchEmbedBlock_0.Dense_0.kernel"] = r(pe_in.reshape(-1, pe_in.shape[-1]).T @ dpe.reshape(-1, C))
+    return float(loss), logits, G

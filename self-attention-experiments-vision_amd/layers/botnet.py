@@ -71,7 +71,11 @@ class BoTMHSA(nn.Module):
     def _build(self, in_ch, device):
         f = self.num_heads * self.head_ch
         bound = math.sqrt(6.0 / in_ch)          # he_uniform: fan_in = 1*1*Cin
-        mk = lambda: nn.Parameter(torch.empty(1, 1, in_ch, f, device=device).uniform_(-bound, bound))
+
+        def mk():   # Flax nn.Conv(kernel_size=(1, 1), use_bias=False): param 'kernel' [1, 1, Cin, h*d]
+            m = nn.Module()
+            m.kernel = nn.Parameter(torch.empty(1, 1, in_ch, f, device=device).uniform_(-bound, bound))
+            return m
         self.query, self.key, self.value = mk(), mk(), mk()
         self._in_ch = in_ch
 
@@ -81,8 +85,8 @@ class BoTMHSA(nn.Module):
             self._build(cin, inputs.device)
         h, d, dt = self.num_heads, self.head_ch, self.dtype
         x = inputs.to(dt).reshape(b, Hs * Ws, cin)
-        w = torch.stack([p.to(dt).reshape(cin, h * d) for p in (self.query, self.key, self.value)], 1)
-        qkv = (x @ w.reshape(cin, 3 * h * d)).view(b, Hs * Ws, 3, h, d)
+        w = [m.kernel.reshape(cin, h * d) for m in (self.query, self.key, self.value)]
+        qkv = ops.dense(x, w, None, dt).view(b, Hs * Ws, 3, h, d)   # the three 1x1 convs as one GEMM
         qhat = qkv[:, :, 0] / math.sqrt(d)                  # botnet.py:185 (head_ch, D1)
         bias = self.RelativeLogits_0.tables(qhat, (Hs, Ws))
         o = ops.attention(qhat, qkv[:, :, 1], qkv[:, :, 2], scale=1.0, bias=bias)

@@ -80,15 +80,18 @@ def test_vit_train_grads_vs_oracle(dev):
     rng = np.random.default_rng(0)
     images = rng.standard_normal((4, 32, 32, 3))
     labels = rng.integers(0, 10, size=4)
-    loss_ref, logits_ref, grads_ref = vit_ref.vit_loss_and_grads(params, images, labels, 2, 2, 8)
+    # the bf16 program of the reference (bf16 rounding points of create_model(dtype=bfloat16) and
+    # the bf16 cotangents of its JAX autodiff), at the stated bf16 bar of 2e-2
+    loss_ref, logits_ref, grads_ref = vit_ref.vit_loss_and_grads_bf16(params, images, labels, 2, 2, 8)
     logits = m(torch.tensor(images, device=dev, dtype=torch.float32), is_training=True)
     loss = train.smoothed_cross_entropy(logits, torch.tensor(labels, device=dev), 0.1)
     loss.backward()
-    assert rel_err(logits.float(), logits_ref) <= 3e-2
-    assert abs(float(loss) - loss_ref) <= 3e-2 * abs(loss_ref)
-    for k, p in m.named_parameters():
-        err = rel_err(p.grad, grads_ref[k])
-        assert err <= 6e-2, f"{k}: rel err {err:.3e}"
+    errs = {k: rel_err(p.grad, grads_ref[k]) for k, p in m.named_parameters()}
+    print("max grad rel err vs bf16 chain:", max(errs.values()), max(errs, key=errs.get))
+    assert rel_err(logits.float(), logits_ref) <= 2e-2
+    assert abs(float(loss) - loss_ref) <= 2e-2 * abs(loss_ref)
+    for k, err in errs.items():
+        assert err <= 2e-2, f"{k}: rel err {err:.3e}"
 
 
 @pytest.mark.parametrize("rowscale", [False, True])
