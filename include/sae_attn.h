@@ -126,9 +126,11 @@ int sae_rotary(void* stream, int32_t batch, int32_t seq, int32_t heads, int32_t 
      P2[i] = sum_h th2[h,i] P[h] ; o = P2 v
    th1/th2 are fp32 [H, H] ([h_in, h_out], talking_heads.py:13).  One workgroup holds one
    query (or key) block for all heads, so heads <= SAE_TH_MAX_HEADS and head_dim <=
-   SAE_TH_MAX_HEAD_DIM (every CaiT config of models/create_model.py:79-150 fits).
+   SAE_TH_MAX_HEAD_DIM: bf16 (16-byte aligned strides) takes up to 16 heads -- every CaiT config
+   of models/create_model.py:79-168, cait_m_24/36/48 included (16 heads, head_dim 48); the fp32
+   (exact) and unaligned paths take up to 8 heads.
    lse: fp32 [B, H, Nq] log-sum-exp of the mixed logits S1 (for the backward). */
-#define SAE_TH_MAX_HEADS 8
+#define SAE_TH_MAX_HEADS 16
 #define SAE_TH_MAX_HEAD_DIM 64
 int sae_th_attn_fwd(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
                     const void* v, const float* th1, const float* th2, void* o, float* lse);

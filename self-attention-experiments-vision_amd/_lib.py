@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("SAE_ATTN_LIB") or os.path.join(_PKG_DIR, "libsae_attn
 SAE_OK, SAE_EINVAL, SAE_EUNSUPPORTED, SAE_EHIP = 0, -1, -2, -3
 SAE_DTYPE_F32, SAE_DTYPE_BF16 = 0, 1
 SAE_FLAG_RELPOS = 1
-SAE_TH_MAX_HEADS = 8
+SAE_TH_MAX_HEADS = 16
 SAE_TH_MAX_HEAD_DIM = 64
 ABI_VERSION = 1
 

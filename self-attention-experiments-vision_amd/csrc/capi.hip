@@ -13,6 +13,7 @@
 #include "../../include/sae_attn.h"
 #include "attn_kernels.h"
 #include "th_kernels.h"
+#include "th2.h"
 #include "variants.h"
 #include "fwd2.h"
 #include "bwd2.h"
@@ -299,8 +300,9 @@ bool th_vec(const sae_attn_desc* d, std::initializer_list<const void*> ptrs, boo
 template <typename T, int DP, bool VEC> int th_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32;
   size_t lds = kTabBytes + 2 * (size_t)a.H * 4096 + (sizeof(T) == 2 ? (size_t)a.H * Img<T, DP>::bytes(32) : 0);
+  if (int rc = lds_attr((const void*)th_fwd_kernel<T, DP, VEC>, lds)) return rc;
   hipLaunchKernelGGL((th_fwd_kernel<T, DP, VEC>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
-  return hipGetLastError() != hipSuccess;
+  return check_launch("th_fwd");
 }
 
 template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a) {
@@ -308,14 +310,46 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
   a.nblk = nqb * a.B;
   size_t lds_q = kTabBytes + 2 * (size_t)a.H * 4096 + (size_t)a.H * 2 * a.H * 64 * sizeof(float) +
                  (sizeof(T) == 2 ? (size_t)a.H * Img<T, DP>::bytes(32) : 0);
+  if (int rc = lds_attr((const void*)th_bwd_q_kernel<T, DP, VEC>, lds_q)) return rc;
   hipLaunchKernelGGL((th_bwd_q_kernel<T, DP, VEC>), dim3(nqb * a.B), dim3(64 * a.H), lds_q, st, a);
-  if (hipGetLastError() != hipSuccess) return 1;
+  if (int rc = check_launch("th_bwd_q")) return rc;
   size_t lds_kv = kTabBytes + 2 * (size_t)a.H * 4096 + (size_t)a.H * 64 * sizeof(float) +
                   (sizeof(T) == 2 ? (size_t)a.H * 2 * Img<T, DP>::bytes(32) : 0);
+  if (int rc = lds_attr((const void*)th_bwd_kv_kernel<T, DP, VEC>, lds_kv)) return rc;
   hipLaunchKernelGGL((th_bwd_kv_kernel<T, DP, VEC>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
-  if (hipGetLastError() != hipSuccess) return 1;
+  if (int rc = check_launch("th_bwd_kv")) return rc;
   hipLaunchKernelGGL(th_reduce_kernel, dim3(2 * a.H * a.H), dim3(256), 0, st, a);
-  return hipGetLastError() != hipSuccess;
+  return check_launch("th_reduce");
+}
+
+// bf16 with the head mixes on the MFMA (th2.h); NWMAX = 8 or 16 waves per workgroup
+template <int DP, int NWMAX> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
+  const int nqb = (a.Nq + 31) / 32;
+  const size_t lds = th2_lds_bytes<DP>(a.H);
+  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX>, lds)) return rc;
+  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  return check_launch("th2_fwd");
+}
+
+template <int DP, int NWMAX> int th2_bwd_run(hipStream_t st, ThArgs a) {
+  const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32;
+  a.nblk = nqb * a.B;
+  const size_t lds = th2_lds_bytes<DP>(a.H), lds_kv = th2_kv_lds_bytes<DP>(a.H, NWMAX <= 8);
+  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX>, lds)) return rc;
+  if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX>, lds_kv)) return rc;
+  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  if (int rc = check_launch("th2_bwd_q")) return rc;
+  hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
+  if (int rc = check_launch("th2_bwd_kv")) return rc;
+  hipLaunchKernelGGL(th_reduce_kernel, dim3(2 * a.H * a.H), dim3(256), 0, st, a);
+  return check_launch("th_reduce");
+}
+
+template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
+  return a.H <= 8 ? th2_fwd_run<DP, 8>(st, a) : th2_fwd_run<DP, 16>(st, a);
+}
+template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
+  return a.H <= 8 ? th2_bwd_run<DP, 8>(st, a) : th2_bwd_run<DP, 16>(st, a);
 }
 
 }  // namespace
@@ -334,6 +368,12 @@ int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
   const bool vec = th_vec(d, {q, k, v, o}, false);
   hipStream_t st = (hipStream_t)stream;
   const int dp = pick_dp(d->head_dim);
+  if (d->dtype == SAE_DTYPE_BF16 && vec) {   // head mixes on the matrix pipe
+    if (dp == 32) return th2_fwd_dispatch<32>(st, a);
+    if (dp == 64) return th2_fwd_dispatch<64>(st, a);
+  }
+  if (d->heads > kThMaxH) return fail(SAE_EUNSUPPORTED, "talking heads: %d heads > %d on the fp32 / unaligned path",
+                                      d->heads, kThMaxH);
 #define TH_F(T, DPV) \
   if (dp == DPV) return vec ? th_fwd_run<T, DPV, true>(st, a) : th_fwd_run<T, DPV, false>(st, a);
   if (d->dtype == SAE_DTYPE_BF16) {
@@ -342,7 +382,7 @@ int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
     TH_F(float, 32) TH_F(float, 64)
   }
 #undef TH_F
-  return 1;
+  return fail(SAE_EUNSUPPORTED, "talking heads: no kernel for dtype %d head_dim %d", d->dtype, d->head_dim);
 }
 
 size_t th_bwd_workspace_bytes(const sae_attn_desc* d) {
@@ -374,6 +414,12 @@ int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
   const bool vec = th_vec(d, {q, k, v, dout, dq, dk, dv}, true);
   hipStream_t st = (hipStream_t)stream;
   const int dp = pick_dp(d->head_dim);
+  if (d->dtype == SAE_DTYPE_BF16 && vec) {
+    if (dp == 32) return th2_bwd_dispatch<32>(st, a);
+    if (dp == 64) return th2_bwd_dispatch<64>(st, a);
+  }
+  if (d->heads > kThMaxH) return fail(SAE_EUNSUPPORTED, "talking heads: %d heads > %d on the fp32 / unaligned path",
+                                      d->heads, kThMaxH);
 #define TH_B(T, DPV) \
   if (dp == DPV) return vec ? th_bwd_run<T, DPV, true>(st, a) : th_bwd_run<T, DPV, false>(st, a);
   if (d->dtype == SAE_DTYPE_BF16) {
@@ -382,7 +428,7 @@ int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
     TH_B(float, 32) TH_B(float, 64)
   }
 #undef TH_B
-  return 1;
+  return fail(SAE_EUNSUPPORTED, "talking heads: no kernel for dtype %d head_dim %d", d->dtype, d->head_dim);
 }
 
 // ==================================================================================== C ABI
@@ -627,7 +673,8 @@ int sae_th_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const v
   if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
     return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
                 SAE_TH_MAX_HEAD_DIM);
-  return th_fwd(stream, d, q, k, v, th1, th2, o, lse) ? fail(SAE_EHIP, "th_fwd launch failed") : check_launch("th_fwd");
+  if (int rc = th_fwd(stream, d, q, k, v, th1, th2, o, lse)) return rc;
+  return ok();
 }
 
 size_t sae_th_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
@@ -646,9 +693,8 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const v
   if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
     return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
                 SAE_TH_MAX_HEAD_DIM);
-  return th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace)
-             ? fail(SAE_EHIP, "th_bwd launch failed")
-             : check_launch("th_bwd");
+  if (int rc = th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace)) return rc;
+  return ok();
 }
 
 // ------------------------------------------------------------------ projection gradients

@@ -1,0 +1,630 @@
+// th2.h -- talking-heads attention (CaiT trunk) for gfx950 with the head mixes on the matrix pipe.
+//
+// Reference: models/layers/attentions/attention.py:41-58 with talking_heads=True and
+// models/layers/attentions/talking_heads.py:9-14 (T is [h_in, h_out]):
+//   S_h = scale Q_h K_h^T ; S1_i = sum_h T1[h,i] S_h ; P_i = softmax_k(S1_i) ;
+//   P2_i = sum_h T2[h,i] P_h ; O_i = P2_i V_i
+// A workgroup owns one 32-row query block (th2_fwd, th2_bwd_q) or one 32-key block (th2_bwd_kv)
+// for ALL H <= 16 heads; wave w computes head w's 32 x 32 score tiles on the MFMA (key on the
+// accumulator rows, query on the lane, as fwd2.h).  The head mix is a tiny [H x H] x [H x 1024]
+// product per tile, done on the MFMA instead of the VALU (th_kernels.h spends 2 x H^2 FMAs per
+// score there):
+//   * every wave writes its tile as bf16 into an exchange image [head][key * 32 + query] (the
+//     reference's scores are bf16 values: attention.py:41-42 returns dtype);
+//   * position block `key` (32 queries) of the tile belongs to wave key mod H, which reads the H
+//     head values of its positions with ds_read_b64_tr_b16 (B operand: 16 heads x 32 positions)
+//     and runs v_mfma_f32_32x32x16_bf16 with A = the [H x H] transform, split into a bf16 high and
+//     low part (two MFMAs: ~16-bit transform precision; the reference promotes the mix to fp32,
+//     talking_heads.py:11-13).  The result has the query on the lane and the mixed head in the
+//     accumulator rows, so the softmax statistics of every (head, query) row live in registers
+//     and the second mix takes the accumulator as its B operand with no lane movement;
+//   * what the next product needs per head goes back through the images.
+// The softmax needs the row statistics of the MIXED logits before P can be mixed again, so the
+// forward sweeps the keys twice (statistics, then output), as the reference's materialised
+// softmax implies.  dT1 / dT2 are 16 x 16 MFMA sums over the score positions of each tile
+// (v_mfma_f32_16x16x32_bf16), reduced over waves and workgroups in a fixed order.
+// bf16 only (the fp32 path keeps th_kernels.h: exact fp32 mixing).
+#pragma once
+#include "common.h"
+#include "th_kernels.h"
+
+namespace sae {
+
+constexpr int kTh2MaxH = 16;
+constexpr int kTh2Row = 2112;                    // bytes per head row: 1024 bf16 + 64 B pad
+constexpr int kTh2Img = kTh2MaxH * kTh2Row;      // one exchange image (33 KiB)
+constexpr int kTh2MixTbl = 4 * 64 * 32;          // th2_bwd_kv: four mix operands (hi, lo) per lane
+
+typedef __attribute__((ext_vector_type(8))) short th_s16x8;
+
+__device__ __forceinline__ bf16x8 th2_tr2(const char* p1, const char* p2) {
+  const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+  const s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
+  const th_s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// A operand of a head mix, high and low bf16 parts: A[row][k] = TR ? T[row][k] : T[k][row]
+// (T fp32 [H][H], [h_in][h_out]).  K order: standard (k = 8 (lane >> 5) + j: the B operand comes
+// from an image) or PERM (the B operand is a 32 x 32 accumulator: element j of lane half g is
+// row 8 (j >> 2) + 4 g + (j & 3)).  Rows / k >= H are zero.
+struct Th2Mix {
+  bf16x8 hi, lo;
+};
+template <bool TR, bool PERM>
+__device__ __forceinline__ Th2Mix th2_mix(const float* T, int H, int lane) {
+  Th2Mix m;
+  const int row = lane & 31, g = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = PERM ? 8 * (j >> 2) + 4 * g + (j & 3) : 8 * g + j;
+    const float t = (row < H && k < H) ? (TR ? T[row * H + k] : T[k * H + row]) : 0.f;
+    const __bf16 hi = (__bf16)t;
+    m.hi[j] = hi;
+    m.lo[j] = (__bf16)(t - (float)hi);
+  }
+  return m;
+}
+
+// mixed tile of position block `blk` (32 positions) from an image: C[row][pos], pos on the lane
+__device__ __forceinline__ f32x16 th2_mix_img(const char* img, int blk, const Th2Mix& m, int lane) {
+  const int li = lane & 15;
+  const int r1 = 8 * (lane >> 5) + (li >> 2);
+  const int col = blk * 32 + 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  const bf16x8 b = th2_tr2(img + r1 * kTh2Row + col * 2, img + (r1 + 4) * kTh2Row + col * 2);
+  f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
+  return MF<__bf16>::mma(m.lo, b, c);
+}
+
+// mixed tile from an accumulator (rows = heads < 16, lanes = positions)
+__device__ __forceinline__ f32x16 th2_mix_acc(const f32x16& x, const Th2Mix& m) {
+  const bf16x8 b = acc_frag<__bf16>(x, 0);
+  f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
+  return MF<__bf16>::mma(m.lo, b, c);
+}
+
+// bf16 tile (accumulator layout: row row_of(r, h) on register r, column on the lane) into image
+// row `head`; every position pos = row * 32 + column.
+__device__ __forceinline__ void th2_put(char* img, int head, const f32x16& v, float sc, int lane) {
+  __bf16* p = reinterpret_cast<__bf16*>(img + head * kTh2Row) + (lane & 31);
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[row_of(r, h) * 32] = (__bf16)(v[r] * sc);
+}
+
+// rows i < H of a mixed block (accumulator rows = heads) into the images at block `blk`
+__device__ __forceinline__ void th2_put_block(char* img, int blk, const f32x16& v, int H, int lane) {
+  __bf16* p = reinterpret_cast<__bf16*>(img) + blk * 32 + (lane & 31);
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = row_of(r, h);
+    if (i < H) p[i * (kTh2Row / 2)] = (__bf16)v[r];
+  }
+}
+
+// zero image rows [H, 16) once (read as the padded k of the mixes; must be finite)
+__device__ __forceinline__ void th2_zero_pad(char* img, int H, int tid, int nthreads) {
+  uint4* p = reinterpret_cast<uint4*>(img + H * kTh2Row);
+  const int n = (kTh2MaxH - H) * kTh2Row / 16;
+  for (int i = tid; i < n; i += nthreads) p[i] = uint4{0, 0, 0, 0};
+}
+
+// 16 x 16 dT partial for position block blk: acc[h = 4 (lane >> 4) + j][i = lane & 15] +=
+// sum over the block's 32 positions of A-image[h] * B-image[i]
+__device__ __forceinline__ f32x4 th2_dt(const char* ia, const char* ib, int blk, f32x4 acc, int lane) {
+  const int row = lane & 15, k0 = blk * 32 + 8 * (lane >> 4);
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(ia + row * kTh2Row + k0 * 2);
+  const bf16x8 b = *reinterpret_cast<const bf16x8*>(ib + row * kTh2Row + k0 * 2);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+
+// B operand of the per-head products, paired with Img::colfrag (K = tile rows in the accumulator
+// order: element j of k-step s, lane half g <-> row 16 s + 8 (j >> 2) + 4 g + (j & 3)).
+// th2_colB: image row `head` read as a [row][column = lane] matrix (position = row * 32 + column),
+// transposed reads.
+__device__ __forceinline__ bf16x8 th2_colB(const char* img, int head, int s, int lane) {
+  const int li = lane & 15;
+  const int r1 = 16 * s + 4 * (lane >> 5) + (li >> 2);
+  const int col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  const char* base = img + head * kTh2Row;
+  return th2_tr2(base + (r1 * 32 + col) * 2, base + ((r1 + 8) * 32 + col) * 2);
+}
+
+// th2_rowB: image row `head` read as a [column = lane][row] matrix (position = column * 32 + row:
+// the key-block kernel, B[k = query][column = key]): two 8-byte reads of query runs
+__device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int lane) {
+  const char* base = img + head * kTh2Row + ((lane & 31) * 32 + 16 * s + 4 * (lane >> 5)) * 2;
+  const s16x4 x1 = *reinterpret_cast<const s16x4*>(base);
+  const s16x4 x2 = *reinterpret_cast<const s16x4*>(base + 16);
+  const th_s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// sum of per-wave 16 x 16 partials (one per wave, in LDS scratch) -> this workgroup's dT slot
+__device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* out, int H, int w, int lane,
+                                             int tid, bool transpose_out) {
+  // acc[j] = dT[h = 4 (lane >> 4) + j][i = lane & 15]
+  f32x4* s4 = reinterpret_cast<f32x4*>(scratch);
+  s4[w * 64 + lane] = acc;
+  __syncthreads();
+  if (tid < 256) {
+    const int ln = tid & 63, j = tid >> 6;   // element j of lane ln: h = 4 (ln >> 4) + j, i = ln & 15
+    float s = 0.f;
+    for (int ww = 0; ww < H; ++ww) s += scratch[(ww * 64 + ln) * 4 + j];
+    const int h = 4 * (ln >> 4) + j, i = ln & 15;
+    if (h < H && i < H) out[transpose_out ? i * H + h : h * H + i] = s;
+  }
+  __syncthreads();
+}
+
+// ================================================================================= forward
+template <int DP, int NWMAX>
+__global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
+  using I = Img<__bf16, DP>;
+  constexpr int NS = DP / 16, NT = DP / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* XS = smem;                          // scores S_h (bf16), then statistics scratch
+  char* XP = smem + kTh2Img;                // mixed probabilities P2_j (bf16)
+  char* ldsV = smem + 2 * kTh2Img + w * I::bytes(32);
+
+  const int nqb = (a.Nq + 31) / 32;
+  const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
+  const int q = qb * 32 + r32;
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
+
+  th2_zero_pad(XS, H, tid, 64 * H);
+  th2_zero_pad(XP, H, tid, 64 * H);
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+  const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);   // S1 = T1^T S
+  const Th2Mix m2 = th2_mix<false, true>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
+  const int nkt = (a.Nk + 31) / 32;
+
+  // ---- pass 0: row statistics (log2 domain) of the mixed logits, per (head i, query) in this
+  //      wave's key blocks: register r <-> head row_of(r, h), lane <-> query
+  float m[8], l[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    m[r] = -kInf;
+    l[r] = 0.f;
+  }
+  // K fragments of the next key tile are loaded while this one computes (the global latency
+  // would otherwise sit in front of every tile's first MFMA)
+  bf16x8 kn[NS];
+  auto load_k = [&](int kt) {
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) kn[s_] = gfrag<__bf16, true>(K, kt * 32 + r32, a.Nk, a.ks[1], a.D, s_, h);
+  };
+  auto scores = [&](int kt) {
+    bf16x8 kc[NS];
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) kc[s_] = kn[s_];
+    load_k(kt + 1 < nkt ? kt + 1 : 0);
+    f32x16 s = zero16();
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) s = MF<__bf16>::mma(kc[s_], qf[s_], s);
+    th2_put(XS, w, s, a.scale, lane);
+  };
+  load_k(0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    scores(kt);
+    __syncthreads();
+    for (int blk = w; blk < 32 && kt * 32 + blk < a.Nk; blk += H) {
+      const f32x16 c = th2_mix_img(XS, blk, m1, lane);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float x = c[r] * kLog2e;
+        const float mn = fmaxf(m[r], x);
+        l[r] = l[r] * ex2(m[r] - mn) + ex2(x - mn);
+        m[r] = mn;
+      }
+    }
+    __syncthreads();
+  }
+  // combine the per-wave statistics: scratch [w][r][lane] (m, l) in the two images
+  {
+    float2* st = reinterpret_cast<float2*>(smem);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st[(w * 8 + r) * 64 + lane] = make_float2(m[r], l[r]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float mm = -kInf, ll = 0.f;
+      for (int ww = 0; ww < H; ++ww) {
+        const float2 v = st[(ww * 8 + r) * 64 + lane];
+        const float mn = fmaxf(mm, v.x);
+        ll = (mm == -kInf ? 0.f : ll * ex2(mm - mn)) + (v.x == -kInf ? 0.f : v.y * ex2(v.x - mn));
+        mm = mn;
+      }
+      m[r] = mm;
+      l[r] = 1.f / ll;   // from here on: 1 / row sum
+      const int i = row_of(r, h);
+      if (w == 0 && i < H && q < a.Nq) a.lse[((size_t)b * H + i) * a.Nq + q] = (mm + lg2(ll)) * kLn2;
+    }
+    __syncthreads();
+    th2_zero_pad(XS, H, tid, 64 * H);   // the scratch overwrote the pad rows
+    th2_zero_pad(XP, H, tid, 64 * H);
+  }
+
+  // ---- pass 1: P_i = 2^(S1 - m) / l, P2 = T2^T P into XP, O_w += P2_w V_w
+  f32x16 acco[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acco[t] = zero16();
+  WStage<__bf16, DP, true> vst;   // V tile kt + 1 in flight while tile kt computes
+  vst.load(V, 0, a.Nk, a.vs[1], a.D, lane);
+  vst.write(ldsV, lane);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) vst.load(V, (kt + 1) * 32, a.Nk, a.vs[1], a.D, lane);
+    scores(kt);
+    __syncthreads();
+    for (int blk = w; blk < 32; blk += H) {
+      f32x16 p2;
+      if (kt * 32 + blk < a.Nk) {
+        f32x16 c = th2_mix_img(XS, blk, m1, lane);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c[r] = ex2(c[r] * kLog2e - m[r]) * l[r];
+#pragma unroll
+        for (int r = 8; r < 16; ++r) c[r] = 0.f;
+        p2 = th2_mix_acc(c, m2);
+      } else {
+        p2 = zero16();   // keys past the end: P2 = 0
+      }
+      th2_put_block(XP, blk, p2, H, lane);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = th2_colB(XP, w, s2, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acco[t] = MF<__bf16>::mma(I::colfrag(ldsV, 0, s2, 32 * t, lane), pf, acco[t]);
+    }
+    if (kt + 1 < nkt) vst.write(ldsV, lane);   // wave-private: after this wave's own reads
+    __syncthreads();
+  }
+  if (q < a.Nq) {
+    __bf16* O = reinterpret_cast<__bf16*>(a.o) + b * a.os[0] + w * a.os[2] + (long long)q * a.os[1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4<__bf16, true>(O, 32 * t + 8 * g + 4 * h, a.D, acco[t][4 * g], acco[t][4 * g + 1], acco[t][4 * g + 2],
+                             acco[t][4 * g + 3]);
+  }
+}
+
+// ============================================================================ bwd: query
+// pass A: delta_i = rowsum(P_i o dP_i), dP = T2 dP2, dP2_j = dO_j V_j^T; dT2 = sum P (x) dP2.
+// pass B: dS1 = P o (dP - delta), dT1 = sum S (x) dS1, dS = T1 dS1, dQ_w += scale dS_w K_w.
+template <int DP, int NWMAX>
+__global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
+  using I = Img<__bf16, DP>;
+  constexpr int NS = DP / 16, NT = DP / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* XS = smem;
+  char* XG = smem + kTh2Img;
+  char* ldsK = smem + 2 * kTh2Img + w * I::bytes(32);
+
+  const int nqb = (a.Nq + 31) / 32;
+  const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
+  const int q = qb * 32 + r32;
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
+  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
+
+  th2_zero_pad(XS, H, tid, 64 * H);
+  th2_zero_pad(XG, H, tid, 64 * H);
+  bf16x8 qf[NS], gf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    gf[s] = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s, h);
+  }
+  const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);    // S1 = T1^T S        (image)
+  const Th2Mix m2t = th2_mix<true, false>(a.th2, H, lane);    // dP = T2 dP2        (image)
+  const Th2Mix m1t = th2_mix<true, true>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
+  // lse (log2 domain) of the mixed rows of this lane's query, register r <-> head row_of(r, h)
+  float lse2[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = row_of(r, h);
+    lse2[r] = (i < H && q < a.Nq) ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
+  }
+  const int nkt = (a.Nk + 31) / 32;
+  bf16x8 kn[NS], vn[NS];   // next key tile's K / V fragments, in flight while this one computes
+  auto load_kv = [&](int kt) {
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) {
+      kn[s_] = gfrag<__bf16, true>(K, kt * 32 + r32, a.Nk, a.ks[1], a.D, s_, h);
+      vn[s_] = gfrag<__bf16, true>(V, kt * 32 + r32, a.Nk, a.vs[1], a.D, s_, h);
+    }
+  };
+  auto tiles = [&](int kt) {   // S_w -> XS, dP2_w -> XG
+    bf16x8 kc[NS], vc[NS];
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) {
+      kc[s_] = kn[s_];
+      vc[s_] = vn[s_];
+    }
+    load_kv(kt + 1 < nkt ? kt + 1 : 0);
+    f32x16 s = zero16(), g = zero16();
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) {
+      s = MF<__bf16>::mma(kc[s_], qf[s_], s);
+      g = MF<__bf16>::mma(vc[s_], gf[s_], g);
+    }
+    th2_put(XS, w, s, a.scale, lane);
+    th2_put(XG, w, g, 1.f, lane);
+  };
+  load_kv(0);
+
+  // ---- pass A
+  float dl[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) dl[r] = 0.f;
+  f32x4 dt2 = {0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < nkt; ++kt) {
+    tiles(kt);
+    __syncthreads();
+    for (int blk = w; blk < 32 && kt * 32 + blk < a.Nk; blk += H) {
+      f32x16 p = th2_mix_img(XS, blk, m1, lane);
+      const f32x16 dp = th2_mix_img(XG, blk, m2t, lane);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        p[r] = ex2(p[r] * kLog2e - lse2[r]);
+        dl[r] += p[r] * dp[r];
+      }
+      th2_put_block(XS, blk, p, H, lane);   // P over S at this block (only this wave touches it)
+      dt2 = th2_dt(XS, XG, blk, dt2, lane);  // dT2[h][i] += sum P_h dP2_i
+    }
+    __syncthreads();
+  }
+  // delta: sum of the per-wave partials (scratch [w][r][lane]) -> registers + workspace
+  {
+    float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st[(w * 8 + r) * 64 + lane] = dl[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float s = 0.f;
+      for (int ww = 0; ww < H; ++ww) s += st[(ww * 8 + r) * 64 + lane];
+      dl[r] = s;
+      const int i = row_of(r, h);
+      if (w == 0 && i < H && q < a.Nq) a.delta[((size_t)b * H + i) * a.Nq + q] = s;
+    }
+    __syncthreads();
+  }
+  float* pb = a.part + (size_t)blockIdx.x * 2 * H * H;
+  th2_dt_store(reinterpret_cast<float*>(smem), dt2, pb + H * H, H, w, lane, tid, false);
+  th2_zero_pad(XS, H, tid, 64 * H);
+  th2_zero_pad(XG, H, tid, 64 * H);   // (the last tile of pass A prefetched key tile 0)
+
+  // ---- pass B
+  f32x16 adq[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) adq[t] = zero16();
+  f32x4 dt1 = {0.f, 0.f, 0.f, 0.f};
+  WStage<__bf16, DP, true> kst;
+  for (int kt = 0; kt < nkt; ++kt) {
+    kst.load(K, kt * 32, a.Nk, a.ks[1], a.D, lane);
+    tiles(kt);
+    kst.write(ldsK, lane);
+    __syncthreads();
+    for (int blk = w; blk < 32; blk += H) {
+      if (kt * 32 + blk < a.Nk) {
+        f32x16 ds1 = th2_mix_img(XS, blk, m1, lane);
+        const f32x16 dp = th2_mix_img(XG, blk, m2t, lane);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ds1[r] = ex2(ds1[r] * kLog2e - lse2[r]) * (dp[r] - dl[r]);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) ds1[r] = 0.f;
+        th2_put_block(XG, blk, ds1, H, lane);   // dS1 over dP2 at this block
+        dt1 = th2_dt(XS, XG, blk, dt1, lane);    // dT1[h][i] += sum S_h dS1_i
+        th2_put_block(XS, blk, th2_mix_acc(ds1, m1t), H, lane);   // dS_h over S_h
+      } else {
+        th2_put_block(XS, blk, zero16(), H, lane);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 sf = th2_colB(XS, w, s2, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) adq[t] = MF<__bf16>::mma(I::colfrag(ldsK, 0, s2, 32 * t, lane), sf, adq[t]);
+    }
+    __syncthreads();
+  }
+  // dT1 partial: XS held the SCALED scores (S = scale q k, the reference's logits)
+  th2_dt_store(reinterpret_cast<float*>(smem), dt1, pb, H, w, lane, tid, false);
+  if (q < a.Nq) {
+    __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + w * a.dqs[2] + (long long)q * a.dqs[1];
+    const float sc = a.scale;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        store4<__bf16, true>(DQ, 32 * t + 8 * g4 + 4 * h, a.D, adq[t][4 * g4] * sc, adq[t][4 * g4 + 1] * sc,
+                             adq[t][4 * g4 + 2] * sc, adq[t][4 * g4 + 3] * sc);
+  }
+}
+
+// =============================================================================== bwd: kv
+// One 32-key block for all heads, sweeping the query tiles: P2 = T2^T P and dS = T1 dS1 per tile
+// (same mixes), dV_w^T += dO_w^T P2_w, dK_w^T += scale Q_w^T dS_w.  The score tiles keep the key
+// on the accumulator rows and the query on the lane, so image position = key * 32 + query and the
+// per-head operands read query runs of a key: plain 16-byte row reads.
+template <int DP, int NWMAX>
+__global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
+  using I = Img<__bf16, DP>;
+  constexpr int NS = DP / 16, NT = DP / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* XS = smem;
+  char* XG = smem + kTh2Img;
+  char* MX = smem + 2 * kTh2Img;   // the four mix operands, per lane (registers are short here)
+  char* buf = MX + kTh2MixTbl + w * I::bytes(32);
+
+  const int nkb = (a.Nk + 31) / 32;
+  const int kb = blockIdx.x % nkb, b = blockIdx.x / nkb;
+  const int key = kb * 32 + r32;
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
+  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
+
+  th2_zero_pad(XS, H, tid, 64 * H);
+  th2_zero_pad(XG, H, tid, 64 * H);
+  bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = gfrag<__bf16, true>(K, key, a.Nk, a.ks[1], a.D, s, h);
+    vf[s] = gfrag<__bf16, true>(V, key, a.Nk, a.vs[1], a.D, s, h);
+  }
+  if (w == 0) {
+    Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
+    mx[0 * 64 + lane] = th2_mix<false, false>(a.th1, H, lane);   // T1^T, image operand
+    mx[1 * 64 + lane] = th2_mix<false, true>(a.th2, H, lane);    // T2^T, accumulator operand
+    mx[2 * 64 + lane] = th2_mix<true, false>(a.th2, H, lane);    // T2, image operand
+    mx[3 * 64 + lane] = th2_mix<true, true>(a.th1, H, lane);     // T1, accumulator operand
+  }
+  const Th2Mix* mx = reinterpret_cast<const Th2Mix*>(MX) + lane;
+  f32x16 adk[NT], adv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    adk[t] = zero16();
+    adv[t] = zero16();
+  }
+  const int nqt = (a.Nq + 31) / 32;
+  // per-wave dO / Q tiles: with <= 8 waves both images stay resident (the S / dP2 operands are read
+  // from them and the next tile is in flight during this one); 16 waves share one 4 KiB buffer
+  // per wave (dO for dV, then Q for dK) and read the S / dP2 operands from global memory
+  constexpr bool TWO = NWMAX <= 8;
+  char* bufQ = TWO ? buf + NWMAX * I::bytes(32) : buf;
+  WStage<__bf16, DP, true> gst, qst;
+  if constexpr (TWO) {
+    gst.load(G, 0, a.Nq, a.dos[1], a.D, lane);
+    qst.load(Q, 0, a.Nq, a.qs[1], a.D, lane);
+    gst.write(buf, lane);
+    qst.write(bufQ, lane);
+  }
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int q = qt * 32 + r32;
+    if constexpr (TWO) {
+      if (qt + 1 < nqt) {
+        gst.load(G, (qt + 1) * 32, a.Nq, a.dos[1], a.D, lane);
+        qst.load(Q, (qt + 1) * 32, a.Nq, a.qs[1], a.D, lane);
+      }
+    } else {
+      gst.load(G, qt * 32, a.Nq, a.dos[1], a.D, lane);
+      qst.load(Q, qt * 32, a.Nq, a.qs[1], a.D, lane);
+    }
+    float lse2[8], dl[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = row_of(r, h);
+      const bool ok = i < H && q < a.Nq;
+      lse2[r] = ok ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
+      dl[r] = ok ? a.delta[((size_t)b * H + i) * a.Nq + q] : 0.f;
+    }
+    {
+      f32x16 s = zero16(), g = zero16();
+#pragma unroll
+      for (int s_ = 0; s_ < NS; ++s_) {
+        bf16x8 qa, ga;
+        if constexpr (TWO) {
+          qa = I::rowfrag(bufQ, r32, s_, h);
+          ga = I::rowfrag(buf, r32, s_, h);
+        } else {
+          qa = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s_, h);
+          ga = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s_, h);
+        }
+        s = MF<__bf16>::mma(kf[s_], qa, s);
+        g = MF<__bf16>::mma(vf[s_], ga, g);
+      }
+      th2_put(XS, w, s, a.scale, lane);
+      th2_put(XG, w, g, 1.f, lane);
+    }
+    if constexpr (!TWO) gst.write(buf, lane);
+    __syncthreads();
+    for (int blk = w; blk < 32; blk += H) {   // blk = key of this block
+      f32x16 p2, ds;
+      if (kb * 32 + blk < a.Nk) {
+        f32x16 p = th2_mix_img(XS, blk, mx[0], lane);
+        const f32x16 dp = th2_mix_img(XG, blk, mx[2 * 64], lane);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) p[r] = ex2(p[r] * kLog2e - lse2[r]);
+        f32x16 ds1;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ds1[r] = p[r] * (dp[r] - dl[r]);
+#pragma unroll
+        for (int r = 8; r < 16; ++r) {
+          p[r] = 0.f;
+          ds1[r] = 0.f;
+        }
+        p2 = th2_mix_acc(p, mx[64]);
+        ds = th2_mix_acc(ds1, mx[3 * 64]);
+      } else {
+        p2 = zero16();
+        ds = zero16();
+      }
+      th2_put_block(XS, blk, p2, H, lane);   // P2_h over S_h at this key
+      th2_put_block(XG, blk, ds, H, lane);   // dS_h over dP2_h
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = th2_rowB(XS, w, s2, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) adv[t] = MF<__bf16>::mma(I::colfrag(buf, 0, s2, 32 * t, lane), pf, adv[t]);
+    }
+    if constexpr (!TWO) qst.write(bufQ, lane);   // one buffer: Q after this wave's own dO reads
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 sf = th2_rowB(XG, w, s2, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) adk[t] = MF<__bf16>::mma(I::colfrag(bufQ, 0, s2, 32 * t, lane), sf, adk[t]);
+    }
+    if constexpr (TWO) {
+      if (qt + 1 < nqt) {   // wave-private images: after this wave's own reads
+        gst.write(buf, lane);
+        qst.write(bufQ, lane);
+      }
+    }
+    __syncthreads();
+  }
+  if (key < a.Nk) {
+    __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + w * a.dks[2] + (long long)key * a.dks[1];
+    __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + w * a.dvs[2] + (long long)key * a.dvs[1];
+    const float sc = a.scale;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * t + 8 * g4 + 4 * h;
+        store4<__bf16, true>(DK, d0, a.D, adk[t][4 * g4] * sc, adk[t][4 * g4 + 1] * sc, adk[t][4 * g4 + 2] * sc,
+                             adk[t][4 * g4 + 3] * sc);
+        store4<__bf16, true>(DV, d0, a.D, adv[t][4 * g4], adv[t][4 * g4 + 1], adv[t][4 * g4 + 2], adv[t][4 * g4 + 3]);
+      }
+  }
+}
+
+// LDS: two exchange images + per-wave 32-row staging (two per wave in th2_bwd_kv at <= 8 waves)
+template <int DP> constexpr size_t th2_lds_bytes(int H) { return 2 * (size_t)kTh2Img + (size_t)H * Img<__bf16, DP>::bytes(32); }
+template <int DP> constexpr size_t th2_kv_lds_bytes(int H, bool two_buffers) {
+  return 2 * (size_t)kTh2Img + kTh2MixTbl + (size_t)(two_buffers ? 16 : H) * Img<__bf16, DP>::bytes(32);
+}
+
+}  // namespace sae

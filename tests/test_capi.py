@@ -91,10 +91,14 @@ def test_talking_heads_envelope():
     from sae_vision_amd import _lib as L
     lib = sae_vision_amd.load_library()
     d = L.SaeAttnDesc()
-    lib.sae_attn_desc_init(ctypes.byref(d), 1, 12, 8, 8, 64, L.SAE_DTYPE_F32, 1.0)
     dummy = ctypes.c_void_p(16)
+    # bf16 (aligned) takes up to SAE_TH_MAX_HEADS = 16 heads (cait_m_*), the fp32 path up to 8
+    lib.sae_attn_desc_init(ctypes.byref(d), 1, 17, 8, 8, 48, L.SAE_DTYPE_BF16, 1.0)
     rc = lib.sae_th_attn_fwd(None, ctypes.byref(d), dummy, dummy, dummy, dummy, dummy, dummy, dummy)
-    assert rc == L.SAE_EUNSUPPORTED and "heads <= 8" in lib.sae_last_error().decode()
+    assert rc == L.SAE_EUNSUPPORTED and "heads <= 16" in lib.sae_last_error().decode()
+    lib.sae_attn_desc_init(ctypes.byref(d), 1, 12, 8, 8, 64, L.SAE_DTYPE_F32, 1.0)
+    rc = lib.sae_th_attn_fwd(None, ctypes.byref(d), dummy, dummy, dummy, dummy, dummy, dummy, dummy)
+    assert rc == L.SAE_EUNSUPPORTED and "12 heads > 8" in lib.sae_last_error().decode()
 
 
 def test_product_path_refuses_cpu_tensors():

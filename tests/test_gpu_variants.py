@@ -31,6 +31,9 @@ def _orth(rng, h):
     (1, 33, 33, 3, 10, "f32"),       # scalar path
     (2, 100, 37, 3, 32, "bf16"),     # CvT talking heads (cvt_attention.py:90-98): Nq != Nk
     (1, 64, 100, 4, 48, "f32"),
+    (2, 196, 196, 16, 48, "bf16"),   # cait_m_24 / _36 / _48: 16 heads (create_model.py:142-168)
+    (1, 70, 45, 12, 48, "bf16"),     # 12 heads, ragged, Nq != Nk
+    (2, 50, 50, 4, 48, "bf16"),      # cait_xxs heads
 ])
 def test_talking_heads(dev, B, N, Nk, H, D, mode):
     import torch

@@ -25,6 +25,7 @@ SHAPES = {  # name: (B, Nq, Nk, H, D)
     "bot14": (256, 196, 196, 4, 128),
     "bot7": (256, 49, 49, 4, 128),
     "cvt1": (64, 3136, 784, 1, 64),
+    "cait_m24": (128, 196, 196, 16, 48),
 }
 
 
@@ -34,6 +35,7 @@ def main():
     ap.add_argument("--shapes", default="deit_s,vitb384,cait_s24,cait_ca,bot14,bot7")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--th", action="store_true", help="talking-heads attention (orthogonal T1, T2)")
     ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B (dev build: SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so)")
     ap.add_argument("--bwd-variants", default="", help="comma list of SAE_BWD_VARIANT values to A/B")
     args = ap.parse_args()
@@ -58,8 +60,16 @@ def main():
         do = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         sc = 1.0 / math.sqrt(D)
-        o, lse = ops._fwd(q, k, v, sc)
-        ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+        if args.th:
+            th1, th2 = (torch.linalg.qr(torch.randn(H, H, device=dev, generator=g))[0].contiguous() for _ in range(2))
+            o, lse, _, _ = ops._th_fwd(q, k, v, th1, th2, sc)
+            fwd_call = lambda: ops._th_fwd(q, k, v, th1, th2, sc)
+            bwd_call = lambda: ops._th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, sc)
+        else:
+            o, lse = ops._fwd(q, k, v, sc)
+            fwd_call = lambda: ops._fwd(q, k, v, sc)
+            bwd_call = lambda: ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+        bwd_call()
         torch.cuda.synchronize()
         # HIP graphs of `reps` back-to-back launches: no host launch gaps inside the timed region
         reps = 10
@@ -67,16 +77,16 @@ def main():
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                ops._fwd(q, k, v, sc)
-                ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+                fwd_call()
+                bwd_call()
         torch.cuda.current_stream().wait_stream(s)
         gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(gf):
             for _ in range(reps):
-                ops._fwd(q, k, v, sc)
+                fwd_call()
         with torch.cuda.graph(gb):
             for _ in range(reps):
-                ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc)
+                bwd_call()
         tf, tb = [], []
         for _ in range(args.iters):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -92,6 +102,9 @@ def main():
         tb.sort()
         mf, mb = tf[len(tf) // 2] / 1e3, tb[len(tb) // 2] / 1e3
         ff, fb = 4.0 * B * H * Nq * Nk * D, 8.0 * B * H * Nq * Nk * D
+        if args.th:   # + the two H x H head mixes: 2 x 2 H^2 Nq Nk fwd, 2 x 4 H^2 Nq Nk bwd
+            ff += 4.0 * B * H * H * Nq * Nk
+            fb += 8.0 * B * H * H * Nq * Nk
         bf = elt * B * H * D * (2 * Nq + 2 * Nk) + 4 * B * H * Nq
         bb = elt * B * H * D * (4 * Nq + 4 * Nk) + 8 * B * H * Nq
         r = {"fwd_us": round(mf * 1e6, 1), "bwd_us": round(mb * 1e6, 1),
