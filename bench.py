@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "attention fwd+bwd TFLOP/s (% MFMA peak); DeiT-S/16 train img/s at 1/8 GPUs"
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA
+PEAK_F32_TFLOPS = 157.3       # MI355X_MICROARCH.md: dense fp32 MFMA
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
 TIMER_STEPS = 3               # graph mode: eager steps timed with HIP events after the timed region
 RIDGE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
@@ -66,14 +67,20 @@ def roofline_entry(flops, nbytes, seconds, traffic=None, bound=None):
             "gbs": round(nbytes / seconds / 1e9, 1), "ms_per_call": round(seconds * 1e3, 4)}
 
 
-def load_traffic(name):
-    """HBM bytes per call from the committed rocprofv3 PMC summary (profiles/), or None."""
+def load_pmc(name, key):
+    """A per-call figure from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    tools/pmc_traffic.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get(name, {}).get("hbm_bytes_per_call")
+            return json.load(f).get(name, {}).get(key)
     except (OSError, ValueError):
         return None
+
+
+def load_traffic(name):
+    """HBM bytes per call (FETCH_SIZE / WRITE_SIZE, gfx950-corrected), or None."""
+    return load_pmc(name, "hbm_bytes_per_call")
 
 
 def cpu_baseline(model_name, seconds_budget=15.0):
@@ -104,22 +111,41 @@ def cpu_baseline(model_name, seconds_budget=15.0):
         if time.perf_counter() - t0 > seconds_budget or n_img >= 16:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(n_img / dt, 3), "unit": "img/s", "cores": int(cores), "kind": "port",
-            "sample": f"{model_name} fp32 numpy train step (fwd+loss+bwd+AdamW), batch {bs} x {n_img // bs} steps, "
-                      f"{dt:.1f} s"}
+    out = {"value": round(n_img / dt, 3), "unit": "img/s", "cores": int(cores), "kind": "port",
+           "affinity_cpus": len(os.sched_getaffinity(0)),
+           "sample": f"{model_name} fp32 numpy train step (fwd+loss+bwd+AdamW), batch {bs} x {n_img // bs} steps, "
+                     f"{dt:.1f} s"}
+    # BASELINE configs[0]: DeiT-Tiny/16 forward + loss on a 224 px batch of 8, the CPU reference path
+    Lt, Ht, Ct, pt = vit.MODEL_CONFIGS["deit_ti_patch16"]
+    ti = vit.create_model("deit_ti_patch16", 1000, torch.float32, device="cpu")
+    pti = {k: v.detach().numpy().astype(np.float32).copy() for k, v in ti.named_parameters()}
+    im8 = rng.standard_normal((8, 224, 224, 3)).astype(np.float32)
+    lb8 = rng.integers(0, 1000, size=8)
+    vit_ref.vit_loss(pti, im8, lb8, Lt, pt)   # warm-up (allocations, BLAS thread pool)
+    n, t1 = 0, time.perf_counter()
+    while n < 3 and time.perf_counter() - t1 < seconds_budget / 3:
+        vit_ref.vit_loss(pti, im8, lb8, Lt, pt)
+        n += 1
+    d1 = (time.perf_counter() - t1) / n
+    out["configs0"] = {"value": round(8 / d1, 3), "unit": "img/s", "ms_per_batch": round(d1 * 1e3, 1),
+                       "cores": int(cores), "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
+                       "sample": f"deit_ti_patch16 224px fp32 numpy forward+loss, batch 8 x {n}"}
+    return out
 
 
-def headline(dev, iters=20, reps=10):
+def headline(dev, iters=20, reps=10, f32=False):
     """Fused attention fwd+bwd alone at the ViT-B/16@384 shape (packed [B, N, 3, H, D] q/k/v as the
     model feeds it).  Each of fwd / bwd is captured as a HIP graph of `reps` back-to-back C-ABI
-    launches; HIP events around each replay on the replay stream; median over `iters` replays."""
+    launches; HIP events around each replay on the replay stream; median over `iters` replays.
+    f32: the fp32 kernels (v_mfma_f32_32x32x2_f32) at batch 16 against the 157.3 TF fp32 MFMA peak."""
     import math
     import torch
     import sae_vision_amd.ops as ops
-    B, N, H, D = 64, 577, 12, 64
+    B, N, H, D = (16 if f32 else 64), 577, 12, 64
+    dt = torch.float32 if f32 else torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    qkv = torch.randn(B, N, 3, H, D, device=dev, generator=g).to(torch.bfloat16)
-    do = torch.randn(B, N, H, D, device=dev, generator=g).to(torch.bfloat16)
+    qkv = torch.randn(B, N, 3, H, D, device=dev, generator=g).to(dt)
+    do = torch.randn(B, N, H, D, device=dev, generator=g).to(dt)
     dqkv = torch.empty_like(qkv)
     sc = 1.0 / math.sqrt(D)
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
@@ -151,10 +177,19 @@ def headline(dev, iters=20, reps=10):
         tf.append(e[0].elapsed_time(e[1]) / reps)
         tb.append(e[1].elapsed_time(e[2]) / reps)
     fwd_ms, bwd_ms = sorted(tf)[iters // 2], sorted(tb)[iters // 2]
-    f_fwd, f_bwd, b_fwd, b_bwd = attn_work(B, N, N, H, D)
+    f_fwd, f_bwd, b_fwd, b_bwd = attn_work(B, N, N, H, D, elt=4 if f32 else 2)
     sec = (fwd_ms + bwd_ms) / 1e3
+    peak = PEAK_F32_TFLOPS if f32 else PEAK_BF16_TFLOPS
+    if f32:
+        tf = (f_fwd + f_bwd) / sec / 1e12
+        return {"shape": {"B": B, "N": N, "H": H, "D": D}, "dtype": "f32", "fwd_ms": round(fwd_ms, 4),
+                "bwd_ms": round(bwd_ms, 4), "tflops": round(tf, 2), "peak": PEAK_F32_TFLOPS,
+                "frac_mfma_peak": round(tf / peak, 4), "timing": f"HIP graphs of {reps} launches, median of {iters}"}
     # BASELINE states the N >= 577 target against the bf16 MFMA peak (AI 286 sits at the ridge)
     r = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, sec, load_traffic("vitb384"), bound="mfma")
+    busy = load_pmc("vitb384", "mfma_busy_frac")
+    if busy is not None:
+        r["mfma_busy_frac"] = busy
     return {"shape": {"B": B, "N": N, "H": H, "D": D}, "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
             "fwd_tflops": round(f_fwd / fwd_ms / 1e9, 1), "bwd_tflops": round(f_bwd / bwd_ms / 1e9, 1),
             "tflops": r["tflops"], "frac_mfma_peak": round(r["tflops"] / PEAK_BF16_TFLOPS, 4),
@@ -175,6 +210,9 @@ def main():
     ap.add_argument("--no-headline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="training loop only (for rocprofv3 runs)")
     ap.add_argument("--eager", action="store_true", help="N=1: eager step instead of the HIP-graph replay")
+    ap.add_argument("--input-layout", default="HWCN", choices=["HWCN", "NHWC"],
+                    help="HWCN: the reference's train-step feed [H, W, C, N] fp32 (train.py:80-81, "
+                         "input_pipeline.py:187-191), gathered by the fused patch GEMM; NHWC: the model call")
     args = ap.parse_args()
 
     import torch
@@ -198,9 +236,11 @@ def main():
     # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1: the
     # eager DDP step (RCCL all-reduce overlapped with the backward through DDP's bucket hooks)
     use_graph = world == 1 and not args.eager
-    step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph)
+    step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph, input_layout=args.input_layout)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
+    if args.input_layout == "HWCN":
+        images = images.permute(1, 2, 3, 0).contiguous()
     labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
     for _ in range(args.warmup):
@@ -249,8 +289,11 @@ def main():
         f_fwd += 2 * 2.0 * B * Hh * Hh * N * N
         f_bwd += 2 * 4.0 * B * Hh * Hh * N * N
     fwd_ms, bwd_ms = ksum[kf]["mean_ms"], ksum[kb]["mean_ms"]
+    is_deit_s = (args.model, args.img_size, B) == ("deit_s_patch16", 224, 128)
     roof = roofline_entry(f_fwd + f_bwd, b_fwd + b_bwd, (fwd_ms + bwd_ms) / 1e3,
-                          load_traffic("deit_s") if (args.model, args.img_size) == ("deit_s_patch16", 224) else None)
+                          load_traffic("deit_s") if is_deit_s else None)
+    if is_deit_s and load_pmc("deit_s", "mfma_busy_frac") is not None:
+        roof["mfma_busy_frac"] = load_pmc("deit_s", "mfma_busy_frac")
     img_s = B * world * args.steps / elapsed
     flop_img = 3 * (cait.cait_flops_per_image(args.model, args.img_size) if is_cait
                     else vit.vit_flops_per_image(args.model, args.img_size))
@@ -266,6 +309,7 @@ def main():
         "config": {"workload": f"{args.model} {args.img_size}px bf16 data-parallel training step (fused attention fwd+bwd)",
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
+                   "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
                    "step": "hip_graph_replay" if use_graph else "eager"},
         "roofline": roof,
         "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,
@@ -278,6 +322,7 @@ def main():
     }
     if not args.profile and not args.no_headline:
         out["attention_headline"] = headline(dev)
+        out["attention_headline_f32"] = headline(dev, iters=5, reps=3, f32=True)
     if not args.profile and not args.no_cpu_baseline and world == 1 and args.img_size == 224 and not is_cait:
         out["cpu_baseline"] = cpu_baseline(args.model)
     print(json.dumps(out), flush=True)

@@ -193,6 +193,34 @@ typedef struct sae_weight_cast_item {
 } sae_weight_cast_item;
 int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* items);
 
+/* Patch embedding (models/layers/stems/patch_embed.py:15-26: einops
+   'b (h ph) (w pw) c -> b (h w) (ph pw c)' then Dense) as one GEMM whose A operand is gathered
+   from the images while it is staged (no patchified copy):
+     out[n][p][e] = sum_k image[n][py*ph + ky][px*pw + kx][c] * wt[e][k] (+ bias[e])
+   with p = py * (width / pw) + px, k = (ky * pw + kx) * channels + c.  images bf16 or fp32
+   (rounded to bf16, train.py:81) in layout SAE_LAYOUT_NHWC [batch][height][width][channels]
+   (the model call) or SAE_LAYOUT_HWCN [height][width][channels][batch] (the train-step feed,
+   train.py:80); wt bf16 [embed][K] (the transposed bf16 kernel, sae_weight_cast), bias fp32
+   [embed] or NULL, out bf16 [batch][L][embed] (L = patches per image).  Requirements:
+   height % ph == width % pw == 0, K = ph*pw*channels a multiple of 64, pw*channels and embed
+   multiples of 8, HWCN batch a multiple of 8, image elements < 2^31, 16-byte aligned pointers. */
+#define SAE_LAYOUT_NHWC 0
+#define SAE_LAYOUT_HWCN 1
+typedef struct sae_patch_desc {
+  int32_t batch, height, width, channels;
+  int32_t patch_h, patch_w, embed;
+  int32_t layout;   /* SAE_LAYOUT_* */
+  int32_t dtype;    /* SAE_DTYPE_BF16 / SAE_DTYPE_F32: the images' element type */
+} sae_patch_desc;
+int sae_patch_embed_fwd(void* stream, const sae_patch_desc* desc, const void* images,
+                        const void* wt, const float* bias, void* out);
+/* Weight / bias gradients of the patch embedding: dw fp32 [K][embed] (+)= sum over tokens of
+   patch[m][k] * dout[m][e], db fp32 [embed] (may be NULL); dout bf16 [batch][L][embed];
+   deterministic split-token reduction through the workspace. */
+size_t sae_patch_embed_bwd_workspace_bytes(const sae_patch_desc* desc);
+int sae_patch_embed_bwd(void* stream, const sae_patch_desc* desc, const void* images,
+                        const void* dout, float* dw, float* db, int32_t accumulate, void* workspace);
+
 /* Residual add + LayerNorm of the encoder blocks around the path (models/vit.py:19-31,57;
    Flax nn.LayerNorm: fp32 statistics, eps, output in the compute dtype):
      xout = x + delta (fp32; when delta != NULL), y = LN(xout) * gamma + beta in bf16,

@@ -93,9 +93,16 @@ def attn_bwd(dy, Wq, Wk, Wv, Wo, cache):
 
 
 def patchify(images, p):
+    """patch_embed.py:19-22, einops 'b (h ph) (w pw) c -> b (h w) (ph pw c)'; p an int or (ph, pw)."""
+    ph, pw = (p, p) if np.isscalar(p) else p
     B, Hh, Ww, c = images.shape
-    x = images.reshape(B, Hh // p, p, Ww // p, p, c).transpose(0, 1, 3, 2, 4, 5)
-    return x.reshape(B, (Hh // p) * (Ww // p), p * p * c)
+    x = images.reshape(B, Hh // ph, ph, Ww // pw, pw, c).transpose(0, 1, 3, 2, 4, 5)
+    return x.reshape(B, (Hh // ph) * (Ww // pw), ph * pw * c)
+
+
+def hwcn_to_nhwc(images):
+    """train.py:80, einops 'H W C N -> N H W C' (the feed's double-transpose layout)."""
+    return np.transpose(images, (3, 0, 1, 2))
 
 
 def smoothed_ce(logits, labels, smoothing, num_classes):
@@ -110,10 +117,9 @@ def smoothed_ce(logits, labels, smoothing, num_classes):
     return loss, dlogits
 
 
-def vit_loss_and_grads(params: Dict[str, np.ndarray], images, labels, num_layers: int, num_heads: int,
-                       patch: int, smoothing: float = 0.1) -> Tuple[float, np.ndarray, Dict[str, np.ndarray]]:
-    """Forward + loss + full backward of ViT (all params).  Returns (loss, logits, grads)."""
-    P = params
+def _vit_forward(P, images, num_layers, patch, keep=True):
+    """models/vit.py:61-99 forward (fp32 numpy): patch embed, [cls] + pos-embed, encoder blocks,
+    final LayerNorm, CLS head.  keep=False drops the backward caches (forward-only timing)."""
     dt = P["cls"].dtype
     B = images.shape[0]
     pe_in = patchify(images.astype(dt), patch)
@@ -132,9 +138,26 @@ def vit_loss_and_grads(params: Dict[str, np.ndarray], images, labels, num_layers
         g = gelu_tanh(u)
         f = g @ P[pre + "FFBlock_0.Dense_1.kernel"] + P[pre + "FFBlock_0.Dense_1.bias"]
         x = x + f
-        caches.append((c1, ca, h2, c2, u, g))
+        if keep:
+            caches.append((c1, ca, h2, c2, u, g))
     z, cz = layer_norm(x, P["Encoder_0.LayerNorm_0.scale"], P["Encoder_0.LayerNorm_0.bias"])
     logits = z[:, 0] @ P["Dense_0.kernel"] + P["Dense_0.bias"]
+    return logits, (pe_in, caches, z, cz)
+
+
+def vit_loss(params: Dict[str, np.ndarray], images, labels, num_layers: int, patch: int,
+             smoothing: float = 0.1) -> float:
+    """Forward + loss only (BASELINE configs[0]: DeiT-Ti forward+loss on the CPU path)."""
+    logits, _ = _vit_forward(params, images, num_layers, patch, keep=False)
+    return float(smoothed_ce(logits, labels, smoothing, logits.shape[-1])[0])
+
+
+def vit_loss_and_grads(params: Dict[str, np.ndarray], images, labels, num_layers: int, num_heads: int,
+                       patch: int, smoothing: float = 0.1) -> Tuple[float, np.ndarray, Dict[str, np.ndarray]]:
+    """Forward + loss + full backward of ViT (all params).  Returns (loss, logits, grads)."""
+    P = params
+    logits, (pe_in, caches, z, cz) = _vit_forward(P, images, num_layers, patch)
+    C = z.shape[-1]
     num_classes = logits.shape[-1]
     loss, dlogits = smoothed_ce(logits, labels, smoothing, num_classes)
 

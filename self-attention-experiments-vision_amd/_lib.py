@@ -28,6 +28,15 @@ _i32, _i64, _f32, _vp, _sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, cty
 _S3 = _i64 * 3
 
 
+SAE_LAYOUT_NHWC, SAE_LAYOUT_HWCN = 0, 1
+
+
+class SaePatchDesc(ctypes.Structure):
+    """Mirror of ``sae_patch_desc`` (include/sae_attn.h)."""
+    _fields_ = [("batch", _i32), ("height", _i32), ("width", _i32), ("channels", _i32),
+                ("patch_h", _i32), ("patch_w", _i32), ("embed", _i32), ("layout", _i32), ("dtype", _i32)]
+
+
 class SaeAttnDesc(ctypes.Structure):
     """Mirror of ``sae_attn_desc`` (include/sae_attn.h)."""
     _fields_ = [
@@ -57,6 +66,9 @@ _PROTOS = [
     ("sae_gemm_dw", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
     ("sae_gemm_dw_blocked", _i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
     ("sae_gemm_nt", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    ("sae_patch_embed_fwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp]),
+    ("sae_patch_embed_bwd_workspace_bytes", _sz, [ctypes.POINTER(SaePatchDesc)]),
+    ("sae_patch_embed_bwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp, _i32, _vp]),
     ("sae_weight_cast", _i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
     ("sae_weight_cast_multi", _i32, [_vp, _i32, _vp]),
     ("sae_layernorm_fwd", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32]),

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from . import ops
 from .layers.attention import ClassSelfAttentionBlock, SelfAttentionBlock
-from .vit import Dense, FFBlock, LayerNorm, encoder_weight_groups
+from .vit import Dense, FFBlock, LayerNorm, encoder_weight_groups, patch_tokens
 
 __all__ = ["CaiT", "create_cait", "CAIT_CONFIGS", "cait_flops_per_image", "LayerScaleBlock",
            "StochasticDepthBlock"]
@@ -213,12 +213,10 @@ class CaiT(nn.Module):
         self.LayerNorm_0 = LayerNorm(embed_dim, device)
         self.Dense_0 = Dense(embed_dim, num_classes, zero_init=True, device=device)
 
-    def forward(self, inputs: torch.Tensor, is_training: bool) -> torch.Tensor:
-        b, H, W, c = inputs.shape
-        ph, pw = self.patch_shape
-        x = inputs.to(self.dtype).reshape(b, H // ph, ph, W // pw, pw, c).permute(0, 1, 3, 2, 4, 5)
-        x = x.reshape(b, (H // ph) * (W // pw), ph * pw * c)
-        x = self.PatchEmbedBlock_0.Dense_0(x, self.dtype)
+    def forward(self, inputs: torch.Tensor, is_training: bool, layout: str = "NHWC") -> torch.Tensor:
+        """``layout`` "HWCN": ``inputs`` is the train-step feed [H, W, C, B] (train.py:80)."""
+        x = patch_tokens(self.PatchEmbedBlock_0, inputs, self.patch_shape, self.dtype, layout)
+        b = x.shape[0]
         x = self.Encoder_0(x, is_training)
         cls_token = self.cls.expand(b, 1, self.embed_dim).float()
         for i in range(self.num_layers_token_only):

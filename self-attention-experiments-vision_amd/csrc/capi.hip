@@ -9,6 +9,7 @@
 #include <initializer_list>
 #include <string>
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/sae_attn.h"
 #include "attn_kernels.h"
@@ -20,6 +21,7 @@
 #include "bwd3.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
+#include "patch.h"
 #include "ln.h"
 
 using namespace sae;
@@ -835,6 +837,149 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
       break;
   }
   return check_launch("gemm_nt");
+}
+
+// ------------------------------------------------------------------------ patch embedding
+static int patch_geom(const sae_patch_desc* d, PatchGeom* g, int* M, int* K) {
+  if (!d) return fail(SAE_EINVAL, "patch_embed: NULL descriptor");
+  if (d->batch < 1 || d->height < 1 || d->width < 1 || d->channels < 1 || d->patch_h < 1 || d->patch_w < 1 ||
+      d->embed < 1)
+    return fail(SAE_EINVAL, "patch_embed: sizes must be >= 1");
+  if (d->layout != SAE_LAYOUT_NHWC && d->layout != SAE_LAYOUT_HWCN)
+    return fail(SAE_EINVAL, "patch_embed: unknown layout %d", d->layout);
+  if (d->dtype != SAE_DTYPE_BF16 && d->dtype != SAE_DTYPE_F32)
+    return fail(SAE_EINVAL, "patch_embed: unknown image dtype %d", d->dtype);
+  if (d->height % d->patch_h || d->width % d->patch_w)
+    return fail(SAE_EINVAL, "patch_embed: image %dx%d is not a whole number of %dx%d patches", d->height, d->width,
+                d->patch_h, d->patch_w);
+  const long long k = (long long)d->patch_h * d->patch_w * d->channels;
+  const long long elems = (long long)d->batch * d->height * d->width * d->channels;
+  const long long L = (long long)(d->height / d->patch_h) * (d->width / d->patch_w);
+  if (k % kNtK || (d->patch_w * d->channels) % 8 || d->embed % 8)
+    return fail(SAE_EUNSUPPORTED, "patch_embed: needs ph*pw*C %% 64 == 0, pw*C %% 8 == 0, embed %% 8 == 0 "
+                "(got K %lld, pw*C %d, embed %d)", k, d->patch_w * d->channels, d->embed);
+  if (d->layout == SAE_LAYOUT_HWCN && d->batch % 8)
+    return fail(SAE_EUNSUPPORTED, "patch_embed: the HWCN layout needs batch %% 8 == 0 (got %d)", d->batch);
+  if (elems >= (1LL << 31) || L * d->batch >= (1LL << 31))
+    return fail(SAE_EUNSUPPORTED, "patch_embed: more than 2^31 image elements or tokens");
+  memset(g, 0, sizeof *g);
+  g->Nb = d->batch;
+  g->Himg = d->height;
+  g->Wimg = d->width;
+  g->C = d->channels;
+  g->Ph = d->patch_h;
+  g->Pw = d->patch_w;
+  g->gw = d->width / d->patch_w;
+  g->L = (int)L;
+  g->PwC = d->patch_w * d->channels;
+  g->WC = d->width * d->channels;
+  g->dL = FDiv::make((unsigned)L);
+  g->dNb = FDiv::make((unsigned)d->batch);
+  g->dgw = FDiv::make((unsigned)g->gw);
+  g->dPwC = FDiv::make((unsigned)g->PwC);
+  *M = (int)(L * d->batch);
+  *K = (int)k;
+  return 0;
+}
+
+extern "C++" {
+template <bool HWCN, bool F32>
+static int patch_fwd_launch(hipStream_t st, const NtArgs& g, long long grid) {
+  const size_t lds = 4 * kNtT * kNtK * 2;
+  const void* fn = (const void*)gemm_nt_kernel<kEpiNone, NtPatchA<HWCN, F32>>;
+  if (int rc = lds_attr(fn, lds)) return rc;
+  hipLaunchKernelGGL((gemm_nt_kernel<kEpiNone, NtPatchA<HWCN, F32>>), dim3((unsigned)grid), dim3(256), lds, st, g);
+  return check_launch("patch_embed_fwd");
+}
+}  // extern "C++"
+
+int sae_patch_embed_fwd(void* stream, const sae_patch_desc* d, const void* images, const void* wt, const float* bias,
+                        void* out) {
+  NtArgs g;
+  memset(&g, 0, sizeof g);
+  int M, K;
+  if (int rc = patch_geom(d, &g.pg, &M, &K)) return rc;
+  if (!images || !wt || !out) return fail(SAE_EINVAL, "patch_embed: images/wt/out must be non-NULL");
+  if (!aligned16(images) || !aligned16(wt) || !aligned16(out) || !aligned16(bias))
+    return fail(SAE_EINVAL, "patch_embed: images, wt, out and bias must be 16-byte aligned");
+  g.pg.x = images;
+  g.bt = reinterpret_cast<const __bf16*>(wt);
+  g.bias = bias;
+  g.c = reinterpret_cast<__bf16*>(out);
+  g.M = M;
+  g.N = d->embed;
+  g.K = K;
+  g.ldb = K;
+  g.ldc = d->embed;
+  const long long grid = (long long)((M + kNtT - 1) / kNtT) * ((d->embed + kNtT - 1) / kNtT);
+  hipStream_t st = (hipStream_t)stream;
+  const bool hwcn = d->layout == SAE_LAYOUT_HWCN, f32 = d->dtype == SAE_DTYPE_F32;
+  int rc = hwcn ? (f32 ? patch_fwd_launch<true, true>(st, g, grid) : patch_fwd_launch<true, false>(st, g, grid))
+                : (f32 ? patch_fwd_launch<false, true>(st, g, grid) : patch_fwd_launch<false, false>(st, g, grid));
+  return rc ? rc : ok();
+}
+
+size_t sae_patch_embed_bwd_workspace_bytes(const sae_patch_desc* d) {
+  PatchGeom g;
+  int M, K;
+  if (patch_geom(d, &g, &M, &K)) return 0;
+  return sae_gemm_dw_workspace_bytes(M, K, d->embed);
+}
+
+extern "C++" {
+template <bool HWCN, bool F32>
+static int patch_dw_launch(hipStream_t st, const DwArgs& a, long long grid) {
+  using YL = typename std::conditional<HWCN, DwPermY, DwRow<true>>::type;
+  const size_t lds = 4 * kDwK * 256;
+  const void* fb = (const void*)gemm_dw_kernel<true, DwPatchX<HWCN, F32>, YL>;
+  const void* fn = (const void*)gemm_dw_kernel<false, DwPatchX<HWCN, F32>, YL>;
+  if (int rc = lds_attr(fb, lds)) return rc;
+  if (int rc = lds_attr(fn, lds)) return rc;
+  if (a.db)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, DwPatchX<HWCN, F32>, YL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((gemm_dw_kernel<false, DwPatchX<HWCN, F32>, YL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  return check_launch("patch_embed_dw");
+}
+}  // extern "C++"
+
+int sae_patch_embed_bwd(void* stream, const sae_patch_desc* d, const void* images, const void* dout, float* dw,
+                        float* db, int32_t accumulate, void* workspace) {
+  DwArgs a;
+  memset(&a, 0, sizeof a);
+  int M, K;
+  if (int rc = patch_geom(d, &a.pg, &M, &K)) return rc;
+  if (!images || !dout || !dw || !workspace)
+    return fail(SAE_EINVAL, "patch_embed_bwd: images/dout/dw/workspace must be non-NULL");
+  if (!aligned16(images) || !aligned16(dout) || !aligned16(dw) || !aligned16(db) || !aligned16(workspace))
+    return fail(SAE_EINVAL, "patch_embed_bwd: images, dout, dw, db and workspace must be 16-byte aligned");
+  const int J = d->embed;
+  a.pg.x = images;
+  a.dy = reinterpret_cast<const __bf16*>(dout);
+  a.M = M;
+  a.I = K;
+  a.J = J;
+  dw_plan(M, K, J, &a.S, &a.chunk);
+  if ((long long)a.chunk * J * 2 >= (1LL << 31))
+    return fail(SAE_EUNSUPPORTED, "patch_embed_bwd: token chunk exceeds 32-bit buffer addressing");
+  a.part = reinterpret_cast<float*>(workspace);
+  a.bpart = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + (((size_t)a.S * K * J * 4 + 255) & ~(size_t)255));
+  a.dw = dw;
+  a.db = db;
+  a.ldy = J;
+  a.ldw = J;
+  a.accumulate = accumulate;
+  hipStream_t st = (hipStream_t)stream;
+  const long long grid = (long long)a.S * ((K + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
+  const bool hwcn = d->layout == SAE_LAYOUT_HWCN, f32 = d->dtype == SAE_DTYPE_F32;
+  int rc = hwcn ? (f32 ? patch_dw_launch<true, true>(st, a, grid) : patch_dw_launch<true, false>(st, a, grid))
+                : (f32 ? patch_dw_launch<false, true>(st, a, grid) : patch_dw_launch<false, false>(st, a, grid));
+  if (rc) return rc;
+  const long long n4 = (long long)K * J / 4;
+  const unsigned rb = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3(rb, db ? 2 : 1), dim3(256), 0, st, a);
+  if (int rc2 = check_launch("patch_embed_dw_reduce")) return rc2;
+  return ok();
 }
 
 int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w16, void* wt16) {

@@ -294,4 +294,33 @@ __device__ __forceinline__ int xcd_remap(int bid, int G) {
 // exact integer key -> (row, col) split for key < 4096, width <= 64: (key * magic) >> 20
 __host__ __device__ inline int div_magic(int w) { return (int)((1u << 20) / (unsigned)w + 1u); }
 
+// Division by a run-time constant d >= 1 for 0 <= n < 2^31 (round-up multiplier, one mul_hi and a
+// shift): q = (mulhi(n, mul) + n) >> sh with sh = ceil(log2 d), mul = floor(2^32 (2^sh - d) / d) + 1.
+struct FDiv {
+  unsigned mul;
+  int sh;
+  __host__ static FDiv make(unsigned d) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    FDiv f;
+    f.mul = (unsigned)((((1ull << l) - d) << 32) / d + 1);
+    f.sh = l;
+    return f;
+  }
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((unsigned)n, mul) + (unsigned)n) >> sh); }
+};
+
+// Patch-embedding geometry (models/layers/stems/patch_embed.py:15-26): the GEMM operand
+// A[m][k] = image[n][py * Ph + ky][px * Pw + kx][c] with k = (ky * Pw + kx) * C + c and token
+// m = (n, p = py * gw + px); `hwcn` selects the train-step feed layout [H, W, C, N]
+// (train.py:80, input_pipeline.py:187-191), whose GEMM row order is m = p * Nb + n (the batch
+// index is the contiguous one there) with output row n * L + p.
+struct PatchGeom {
+  const void* x;                 // images, bf16 or fp32
+  int Nb, Himg, Wimg, C, Ph, Pw;
+  int gw, L;                     // patches per image row, patches per image
+  int PwC, WC;                   // Pw * C (one patch row), Wimg * C (one image row)
+  FDiv dL, dNb, dgw, dPwC;
+};
+
 }  // namespace sae

@@ -33,6 +33,7 @@ struct DwArgs {
   long long ldx, ldy, ldw;
   int accumulate;     // dw / db += instead of =
   int jblock;         // > 0: dw is [J / jblock][I][jblock] (column blocks contiguous), ldw unused
+  PatchGeom pg;       // patch-embedding X operand (patch.h), unused otherwise
 };
 
 constexpr int kDwT = 128;   // output tile edge
@@ -64,6 +65,25 @@ struct DwStage {
   }
 };
 
+// Operand loaders of the plain kernel: token rows [m0, m1) of the row-major x [M][I] / dy [M][J]
+// through buffer descriptors (rows past m1 read zero), columns col0 .. col0 + 127.  patch.h
+// supplies the patch-gather loaders.
+template <bool Y>
+struct DwRow {
+  DwStage<4> s;
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned step;
+  __device__ __forceinline__ void init(const DwArgs& a, int tid, int m0, int m1, int col0) {
+    const __bf16* base = Y ? a.dy : a.x;
+    const long long ld = Y ? a.ldy : a.ldx;
+    rs = row_rsrc(base + (long long)m0 * ld, m1 - m0, ld);
+    s.init(tid, ld, col0, Y ? a.J : a.I);
+    step = (unsigned)(kDwK * ld * 2);
+  }
+  __device__ __forceinline__ void load(const DwArgs&, int st) { s.load(rs, (unsigned)st * step); }
+  __device__ __forceinline__ void write(char* img) const { s.write(img); }
+};
+
 // transposed operand read: column col0 + (lane & 31) on the lane, K over rows 16s + permuted
 __device__ __forceinline__ bf16x8 dw_colfrag(const char* img, const unsigned* ca, int s, int t) {
   typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -74,7 +94,7 @@ __device__ __forceinline__ bf16x8 dw_colfrag(const char* img, const unsigned* ca
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <bool BIAS>
+template <bool BIAS, class XL = DwRow<false>, class YL = DwRow<true>>
 __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int IMG = kDwK * 256;     // 16 KiB per operand image
@@ -93,26 +113,23 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   const int m1 = min(a.M, m0 + a.chunk);
   const bool bias = BIAS && it == 0 && wi == 0;
 
-  // row ranges [m0, m1) of X and dY through buffer descriptors (rows past m1 read zero)
-  const __amdgpu_buffer_rsrc_t rx = row_rsrc(a.x + (long long)m0 * a.ldx, m1 - m0, a.ldx);
-  const __amdgpu_buffer_rsrc_t ry = row_rsrc(a.dy + (long long)m0 * a.ldy, m1 - m0, a.ldy);
   // two register stages in flight: the loads for stage st + 2 are issued while stage st computes
   // and stage st + 1 (issued one stage earlier) is written to LDS at its end
-  DwStage<4> xs[2], ys[2];
+  XL xs[2];
+  YL ys[2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    xs[r].init(tid, a.ldx, i0, a.I);
-    ys[r].init(tid, a.ldy, j0, a.J);
+    xs[r].init(a, tid, m0, m1, i0);
+    ys[r].init(a, tid, m0, m1, j0);
   }
-  const unsigned xstep = (unsigned)(kDwK * a.ldx * 2), ystep = (unsigned)(kDwK * a.ldy * 2);
   const int nst = (m1 - m0 + kDwK - 1) / kDwK;
   // straight-line staging (as gemm_nt.h): stage loads / LDS writes past the end are issued
-  // unconditionally (they read zeros: the descriptors end at m1) so the waitcnt pass keeps two
+  // unconditionally (they read zeros: rows past m1 are zero) so the waitcnt pass keeps two
   // register stages in flight instead of draining the queue before every reload
-  xs[0].load(rx, 0);
-  ys[0].load(ry, 0);
-  xs[1].load(rx, xstep);
-  ys[1].load(ry, ystep);
+  xs[0].load(a, 0);
+  ys[0].load(a, 0);
+  xs[1].load(a, 1);
+  ys[1].load(a, 1);
 
   unsigned ca[8];   // [operand x / dy][t = 0, 1][r1, r2] transposed-read addresses
   {
@@ -166,8 +183,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
       const char* imx = smem + bsel * 2 * IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
       // register set bsel was written to LDS at the end of the previous stage: refill (stage + 2)
-      xs[bsel].load(rx, (unsigned)(st + bsel + 2) * xstep);
-      ys[bsel].load(ry, (unsigned)(st + bsel + 2) * ystep);
+      xs[bsel].load(a, st + bsel + 2);
+      ys[bsel].load(a, st + bsel + 2);
       compute(imx, imx + IMG);
       xs[bsel ^ 1].write(nxt);
       ys[bsel ^ 1].write(nxt + IMG);

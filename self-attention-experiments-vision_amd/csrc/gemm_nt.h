@@ -36,6 +36,7 @@ struct NtArgs {
   __bf16* c2;          // [M][N] row stride ldc (kEpiGelu: pre-activation)
   int M, N, K;
   long long lda, ldb, ldc, ldaux;
+  PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
 };
 
 constexpr int kNtT = 128;   // output tile edge
@@ -111,7 +112,22 @@ struct NtStage {
   }
 };
 
-template <int EPI>
+// A-operand loader of the plain GEMM: rows m0 .. m0 + 127 of the row-major a [M][K] through a
+// buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders; a loader
+// also maps GEMM row m to its output row (orow).
+struct NtRowA {
+  NtStage s;
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ void init(const NtArgs& a, int tid, int m0) {
+    rs = row_rsrc(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
+    s.init(tid, a.lda);
+  }
+  __device__ __forceinline__ void load(const NtArgs&, int st) { s.load(rs, (unsigned)st * (kNtK * 2)); }
+  __device__ __forceinline__ void write(char* img) const { s.write(img); }
+  static __device__ __forceinline__ long long orow(const NtArgs&, int m) { return m; }
+};
+
+template <int EPI, class AL = NtRowA>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int IMG = kNtT * kNtK * 2;   // 16 KiB per operand image
@@ -123,13 +139,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w & 1, wn = w >> 1;   // this wave's 64 (tokens) x 64 (features) quarter
 
-  // rows past M / N read zero through the descriptors' range checks
-  const __amdgpu_buffer_rsrc_t ra = row_rsrc(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
+  // rows past N read zero through the descriptor's range check
   const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
-  NtStage as[2], bs[2];
+  AL as[2];
+  NtStage bs[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    as[q].init(tid, a.lda);
+    as[q].init(a, tid, m0);
     bs[q].init(tid, a.ldb);
   }
   const int nst = a.K / kNtK;
@@ -138,9 +154,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   // past the end they read zeros (descriptor range check) or unused bytes into a buffer nobody
   // reads again -- so the waitcnt pass can prove each register set's loads retired and keeps two
   // stages in flight (with conditional loads it waited vmcnt(0) before every reload).
-  as[0].load(ra, 0);
+  as[0].load(a, 0);
   bs[0].load(rb, 0);
-  as[1].load(ra, kNtK * 2);
+  as[1].load(a, 1);
   bs[1].load(rb, kNtK * 2);
   // kEpiDGelu: this lane's eight aux chunks (the epilogue's row groups) are loaded before the
   // main loop, so their HBM traffic overlaps the MFMAs instead of following them
@@ -153,7 +169,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int m = m0 + 64 * wm + 32 * u + 8 * it + (lane >> 3);
-        auxv[u][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n)
+        auxv[u][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + AL::orow(a, m) * a.ldaux + n)
                                            : uint4{0, 0, 0, 0};
       }
   }
@@ -186,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
       const char* ima = smem + bsel * 2 * IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
       // register set bsel went to LDS at the end of the previous stage: refill it (stage + 2)
-      as[bsel].load(ra, (unsigned)(st + bsel + 2) * (kNtK * 2));
+      as[bsel].load(a, st + bsel + 2);
       bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (kNtK * 2));
       compute(ima, ima + IMG);
       as[bsel ^ 1].write(nxt);
@@ -234,17 +250,18 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
       const int m = m0 + 64 * wm + 32 * u + rr;
       const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * 128 + 16 * (c8 ^ swz<64>(rr)));
       if (m < a.M && n < a.N) {
+        const long long orow = AL::orow(a, m);
         if constexpr (EPI == kEpiNone) {
-          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
+          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = raw;
         } else if constexpr (EPI == kEpiGelu) {
-          *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
+          *reinterpret_cast<uint4*>(a.c2 + orow * a.ldc + n) = raw;
           const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
-          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;
         } else {
           const uint4 hv = auxv[u][it];
           const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
                            dgelu_bf2(raw.w, hv.w)};
-          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;
         }
       }
     }

@@ -554,6 +554,86 @@ def dense(x: torch.Tensor, w, b: Optional[torch.Tensor], dtype: torch.dtype) -> 
     return _Dense.apply(x, b, dtype, *ws)
 
 
+# ------------------------------------------------------------------------- patch embedding
+def _patch_desc(images: torch.Tensor, patch: Tuple[int, int], embed: int, layout: str) -> L.SaePatchDesc:
+    if layout == "NHWC":
+        B, H, W, C = images.shape
+        code = L.SAE_LAYOUT_NHWC
+    elif layout == "HWCN":
+        H, W, C, B = images.shape
+        code = L.SAE_LAYOUT_HWCN
+    else:
+        raise ValueError(f"patch_embed: layout must be 'NHWC' or 'HWCN', got {layout!r}")
+    return L.SaePatchDesc(B, H, W, C, int(patch[0]), int(patch[1]), int(embed), code, dtype_code(images.dtype))
+
+
+class _PatchEmbed(torch.autograd.Function):
+    """patch_embed.py:15-26 in bf16: the patch gather fused into the GEMM's operand staging
+    (``sae_patch_embed_fwd``), weight / bias gradients by the same gather (``sae_patch_embed_bwd``).
+    The images take no gradient (they are the batch, train.py:80-82)."""
+
+    @staticmethod
+    def forward(ctx, images, w, b, patch, layout):
+        lib = L.load()
+        E = w.shape[1]
+        desc = _patch_desc(images, patch, E, layout)
+        _, wt = _cast([w], torch.bfloat16)
+        Lp = (desc.height // desc.patch_h) * (desc.width // desc.patch_w)
+        out = torch.empty((desc.batch, Lp, E), dtype=torch.bfloat16, device=images.device)
+        bias = b.float().contiguous() if b is not None else None
+        tok = _TIMER.begin("patch_embed") if _TIMER is not None else None
+        L.check(lib.sae_patch_embed_fwd(_stream(images), ctypes.byref(desc), _ptr(images), _ptr(wt), _ptr(bias),
+                                        _ptr(out)))
+        if tok is not None:
+            _TIMER.end(tok, (desc.batch * Lp, w.shape[0], E))
+        ctx.save_for_backward(images)
+        ctx.desc, ctx.wshape, ctx.wdtype, ctx.has_b = desc, tuple(w.shape), w.dtype, b is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = L.load()
+        (images,) = ctx.saved_tensors
+        desc = ctx.desc
+        dout = dout.to(torch.bfloat16).contiguous()
+        dw = torch.empty(ctx.wshape, dtype=torch.float32, device=dout.device)
+        db = torch.empty((ctx.wshape[1],), dtype=torch.float32, device=dout.device) if ctx.has_b else None
+        ws = torch.empty(lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8,
+                         device=dout.device)
+        L.check(lib.sae_patch_embed_bwd(_stream(dout), ctypes.byref(desc), _ptr(images), _ptr(dout), _ptr(dw),
+                                        _ptr(db), 0, _ptr(ws)))
+        return None, dw.to(ctx.wdtype), db, None, None
+
+
+def patch_embed(images: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], patch: Tuple[int, int],
+                layout: str = "NHWC") -> torch.Tensor:
+    """``PatchEmbedBlock`` (patch_embed.py:15-26) in bf16: tokens [B, L, E] of ``images`` (bf16 or
+    fp32; ``layout`` "NHWC" [B, H, W, C] or the train-step feed "HWCN" [H, W, C, B], train.py:80)
+    times the fp32 Dense kernel ``w`` [ph * pw * C, E] (+ ``b``).  The images take no gradient."""
+    _require_gpu(images, w)
+    if images.requires_grad:
+        raise NotImplementedError("patch_embed: the images take no gradient on this path (train.py:80-82)")
+    if images.dtype not in (torch.bfloat16, torch.float32):
+        images = images.float()
+    if not images.is_contiguous() or images.data_ptr() % 16:
+        images = images.contiguous()
+    if w.dtype != torch.float32 or w.dim() != 2:
+        raise ValueError("patch_embed: w must be the fp32 Dense kernel [ph * pw * C, E]")
+    return _PatchEmbed.apply(images, w, b, tuple(int(p) for p in patch), layout)
+
+
+def patch_embed_ok(images: torch.Tensor, w: torch.Tensor, patch: Tuple[int, int], layout: str = "NHWC") -> bool:
+    """Shapes the fused kernel takes (sae_patch_embed_fwd's requirements, include/sae_attn.h)."""
+    if images.dim() != 4 or not images.is_cuda:
+        return False
+    H, W, C, B = images.shape if layout == "HWCN" else (images.shape[1], images.shape[2], images.shape[3],
+                                                        images.shape[0])
+    ph, pw = patch
+    K = ph * pw * C
+    return (H % ph == 0 and W % pw == 0 and K % 64 == 0 and (pw * C) % 8 == 0 and w.shape[1] % 8 == 0
+            and w.shape[0] == K and (layout != "HWCN" or B % 8 == 0))
+
+
 # ------------------------------------------------- forward / input-gradient GEMMs (sae_gemm_nt)
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 

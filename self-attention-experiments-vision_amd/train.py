@@ -53,7 +53,10 @@ class TrainStep:
 
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
                  label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
-                 graph: bool = False):
+                 graph: bool = False, input_layout: str = "NHWC"):
+        # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
+        # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
+        self.input_layout = input_layout
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         # One HIP graph for the whole step (forward, loss, backward, AdamW): the eager step spends
         # ~10 ms/step of host time submitting ~600 launches (tools/ab_step.py), as long as the GPU
@@ -81,7 +84,10 @@ class TrainStep:
 
     def _eager(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         self.opt.zero_grad(set_to_none=True)
-        logits = self.ddp(images, is_training=True)
+        if self.input_layout == "NHWC":
+            logits = self.ddp(images, is_training=True)
+        else:
+            logits = self.ddp(images, is_training=True, layout=self.input_layout)
         loss = smoothed_cross_entropy(logits, labels, self.smoothing)
         loss.backward()
         self.opt.step()

@@ -139,6 +139,24 @@ class Encoder(nn.Module):
         return self.LayerNorm_0(x, self.dtype)
 
 
+def patch_tokens(pe: nn.Module, inputs: torch.Tensor, patch_shape: Tuple[int, int], dtype: torch.dtype,
+                 layout: str = "NHWC") -> torch.Tensor:
+    """``PatchEmbedBlock_0`` (patch_embed.py:15-26) of ``inputs`` in the model call layout
+    "NHWC" [B, H, W, C] or the train-step feed "HWCN" [H, W, C, B] (train.py:80): in bf16 one
+    fused patch-gather GEMM (``ops.patch_embed``); otherwise (fp32 compute, shapes the kernel
+    does not take) the einops rearrange and a Dense."""
+    w = pe.Dense_0.kernel
+    if dtype == torch.bfloat16 and ops.patch_embed_ok(inputs, w, patch_shape, layout):
+        return ops.patch_embed(inputs, w, pe.Dense_0.bias, patch_shape, layout)
+    if layout == "HWCN":
+        inputs = inputs.permute(3, 0, 1, 2)                        # 'H W C N -> N H W C'
+    b, H, W, c = inputs.shape
+    ph, pw = patch_shape
+    x = inputs.to(dtype).reshape(b, H // ph, ph, W // pw, pw, c).permute(0, 1, 3, 2, 4, 5)
+    x = x.reshape(b, (H // ph) * (W // pw), ph * pw * c)          # 'b (h ph) (w pw) c -> b (h w) (ph pw c)'
+    return pe.Dense_0(x, dtype)
+
+
 class ViT(nn.Module):
     """vit.py:61-99.  ``forward(inputs [B, H, W, 3], is_training)`` -> logits [B, classes]."""
 
@@ -156,12 +174,10 @@ class ViT(nn.Module):
         self.Encoder_0 = Encoder(n, embed_dim, num_layers, num_heads, expand_ratio, dtype, device)
         self.Dense_0 = Dense(embed_dim, num_classes, zero_init=True, device=device)
 
-    def forward(self, inputs: torch.Tensor, is_training: bool) -> torch.Tensor:
-        b, H, W, c = inputs.shape
-        ph, pw = self.patch_shape
-        x = inputs.to(self.dtype).reshape(b, H // ph, ph, W // pw, pw, c).permute(0, 1, 3, 2, 4, 5)
-        x = x.reshape(b, (H // ph) * (W // pw), ph * pw * c)          # 'b (h ph) (w pw) c -> b (h w) (ph pw c)'
-        x = self.PatchEmbedBlock_0.Dense_0(x, self.dtype)
+    def forward(self, inputs: torch.Tensor, is_training: bool, layout: str = "NHWC") -> torch.Tensor:
+        """``layout`` "HWCN": ``inputs`` is the train-step feed [H, W, C, B] (train.py:80)."""
+        x = patch_tokens(self.PatchEmbedBlock_0, inputs, self.patch_shape, self.dtype, layout)
+        b = x.shape[0]
         x = torch.cat([self.cls.expand(b, 1, self.embed_dim), x.float()], dim=1)   # fp32 (promotion)
         x = self.Encoder_0(x, is_training)
         return self.Dense_0(x[:, 0], self.dtype)

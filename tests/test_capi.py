@@ -119,3 +119,24 @@ def test_missing_library_fails_loudly(tmp_path):
             L.load(str(tmp_path / "nope.so"))
     finally:
         L._lib = old
+
+
+def test_patch_embed_validation():
+    """sae_patch_desc layout and the host-side shape checks of the patch-embedding entry points."""
+    import sae_vision_amd
+    from sae_vision_amd import _lib as L
+    lib = sae_vision_amd.load_library()
+    assert ctypes.sizeof(L.SaePatchDesc) == 9 * 4
+    dummy = ctypes.c_void_p(16)
+    cases = [
+        (L.SaePatchDesc(12, 32, 32, 3, 16, 16, 384, L.SAE_LAYOUT_HWCN, L.SAE_DTYPE_BF16), "batch % 8"),
+        (L.SaePatchDesc(8, 40, 32, 3, 16, 16, 384, L.SAE_LAYOUT_NHWC, L.SAE_DTYPE_BF16), "whole number"),
+        (L.SaePatchDesc(8, 30, 30, 3, 10, 10, 384, L.SAE_LAYOUT_NHWC, L.SAE_DTYPE_BF16), "% 64"),
+        (L.SaePatchDesc(8, 32, 32, 3, 16, 16, 384, 5, L.SAE_DTYPE_BF16), "layout 5"),
+    ]
+    for d, msg in cases:
+        rc = lib.sae_patch_embed_fwd(None, ctypes.byref(d), dummy, dummy, None, dummy)
+        assert rc != L.SAE_OK and msg in lib.sae_last_error().decode(), (msg, lib.sae_last_error())
+        assert lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(d)) == 0
+    ok = L.SaePatchDesc(128, 224, 224, 3, 16, 16, 384, L.SAE_LAYOUT_HWCN, L.SAE_DTYPE_F32)
+    assert lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(ok)) > 0

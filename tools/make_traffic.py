@@ -4,7 +4,8 @@
 usage: python tools/make_traffic.py <name>=<pmc_outdir> [...]
 Per kernel: hbm = FETCH_SIZE*1024*2 (gfx950: FETCH_SIZE counts half of a wide coalesced
 stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE*1024, averaged over dispatches; one call =
-attn_fwd2 + attn_bwd2_dq + attn_bwd2_dkdv (bf16, head_dim 64 instances).
+attn_fwd2 + attn_bwd3 (Nk <= 256) or attn_bwd2_dq + attn_bwd2_dkdv (bf16, head_dim 64 instances);
+mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), time-weighted.
 """
 import json
 import os
@@ -14,7 +15,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import main as summarize  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("attn_fwd2_kernel<64", "attn_bwd2_dq_kernel<64", "attn_bwd2_dkdv_kernel<64")   # bf16, head_dim 64
+# bf16, head_dim 64: forward + (single-pass bwd3 for Nk <= 256 | two-pass bwd2 dq + dkdv)
+KERNELS = ("attn_fwd2_kernel<64", "attn_bwd3_kernel<64", "attn_bwd2_dq_kernel<64", "attn_bwd2_dkdv_kernel<64")
+SIMDS = 1024          # 256 CUs x 4 SIMDs
+XCDS = 8              # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
 
 
 def main(args):
@@ -30,8 +34,17 @@ def main(args):
                 continue
             v = max(rows, key=lambda r: r.get("FETCH_SIZE", 0))
             per[k] = {"fetch_bytes": v["FETCH_SIZE"] * 1024 * 2, "write_bytes": v["WRITE_SIZE"] * 1024}
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in v and "GRBM_GUI_ACTIVE" in v:
+                cyc = v["GRBM_GUI_ACTIVE"] / XCDS
+                per[k].update(mfma_busy_cycles=v["SQ_VALU_MFMA_BUSY_CYCLES"], cycles=cyc,
+                              mfma_busy_frac=round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS), 4))
         data[name] = {"hbm_bytes_per_call": sum(x["fetch_bytes"] + x["write_bytes"] for x in per.values()),
                       "per_kernel": per, "source": d}
+        if per and all("cycles" in x for x in per.values()):
+            # MFMA pipe busy over the call (time-weighted; SQ_VALU_MFMA_BUSY_CYCLES counts the
+            # issued MFMA cycles of every SIMD: busy / (duration cycles x 1024 SIMDs))
+            data[name]["mfma_busy_frac"] = round(sum(x["mfma_busy_cycles"] for x in per.values())
+                                                 / (sum(x["cycles"] for x in per.values()) * SIMDS), 4)
     json.dump(data, open(path, "w"), indent=1)
     print(json.dumps(data, indent=1))
 
