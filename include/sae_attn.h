@@ -121,6 +121,21 @@ int sae_rotary(void* stream, int32_t batch, int32_t seq, int32_t heads, int32_t 
                const int64_t y_stride[3], const float* sin_tab, const float* cos_tab,
                int32_t inverse);
 
+/* Attention with the rotary embedding fused (position_embed.py:8-20 applied to q and k before
+   the scores): q and k are passed UN-rotated and rotated by the kernels as they are staged
+   (sin/cos fp32 [max(seq_q, seq_k)][head_dim / 2], row = position), so the rotated tensors
+   never exist in memory; the backward returns dq / dk for the un-rotated q / k (rotated back
+   as they are stored).  Bit-identical to sae_rotary + sae_attn_fwd / sae_attn_bwd + sae_rotary
+   (inverse).  bf16, 16-byte aligned strides, head_dim % 8 == 0 (backward: head_dim <= 64),
+   no flags; otherwise SAE_EUNSUPPORTED (use sae_rotary + the plain entry points). */
+int sae_attn_fwd_rotary(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                        const void* v, const float* sin_tab, const float* cos_tab, void* o,
+                        float* lse);
+int sae_attn_bwd_rotary(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                        const void* v, const void* o, const float* lse, const void* dout,
+                        const float* sin_tab, const float* cos_tab, void* dq, void* dk, void* dv,
+                        void* workspace);
+
 /* Talking-heads attention (attention.py:41-58 with talking_heads=True):
      S = scale q k^T ; S1[i] = sum_h th1[h,i] S[h] ; P = softmax(S1) ;
      P2[i] = sum_h th2[h,i] P[h] ; o = P2 v
@@ -143,6 +158,15 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* desc, const void* q, cons
                     const void* v, const float* th1, const float* th2, const float* lse,
                     const void* dout, void* dq, void* dk, void* dv, float* dth1,
                     float* dth2, void* workspace);
+
+/* Talking heads with the rotary embedding fused (as sae_attn_fwd_rotary; bf16, aligned). */
+int sae_th_attn_fwd_rotary(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                           const void* v, const float* th1, const float* th2,
+                           const float* sin_tab, const float* cos_tab, void* o, float* lse);
+int sae_th_attn_bwd_rotary(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
+                           const void* v, const float* th1, const float* th2, const float* lse,
+                           const void* dout, const float* sin_tab, const float* cos_tab, void* dq,
+                           void* dk, void* dv, float* dth1, float* dth2, void* workspace);
 
 /* Weight / bias gradients of a projection on the path (the Dense / DenseGeneral kernels of
    attention.py:29-37,60-63 and ff.py:8-34, whose JAX autodiff computes them):

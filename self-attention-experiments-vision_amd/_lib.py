@@ -62,6 +62,10 @@ _PROTOS = [
     ("sae_th_attn_fwd", _i32, [_vp, ctypes.POINTER(SaeAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("sae_th_attn_bwd_workspace_bytes", _sz, [ctypes.POINTER(SaeAttnDesc)]),
     ("sae_th_attn_bwd", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 13),
+    ("sae_attn_fwd_rotary", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 7),
+    ("sae_attn_bwd_rotary", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 12),
+    ("sae_th_attn_fwd_rotary", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 9),
+    ("sae_th_attn_bwd_rotary", _i32, [_vp, ctypes.POINTER(SaeAttnDesc)] + [_vp] * 15),
     ("sae_gemm_dw_workspace_bytes", _sz, [_i32, _i32, _i32]),
     ("sae_gemm_dw", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
     ("sae_gemm_dw_blocked", _i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),

@@ -44,6 +44,7 @@ struct AttnArgs {
   long long qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
   float scale;
   int rel_h, rel_w, rel_magic;
+  RopeTab rope;     // rotary tables (the ROT kernel instances), rope.sin == nullptr otherwise
 };
 
 constexpr int kBQ = 128;   // query rows per forward / dq workgroup (4 waves x 32)

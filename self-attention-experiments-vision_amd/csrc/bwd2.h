@@ -19,7 +19,8 @@ namespace sae {
 // delta = rowsum(dO o O) is computed from the fragments in registers and published for the
 // dK/dV pass.  Per 32-key half: S^T = K Q^T, dP^T = V dO^T (row reads of the K / V images),
 // dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T (transposed reads of the K image).
-template <int DP, int NW, int MINW>
+// ROT (both passes): q / k rotated as they are staged, dq / dk rotated back as they are stored.
+template <int DP, int NW, int MINW, bool ROT = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -74,6 +75,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)gf[s][j];
     }
     dlt = xhalf_sum(part);
+    if constexpr (ROT) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
+    }
   }
   const bool qok = q < a.Nq;
   if (qok && h == 0) a.delta[rowoff + q] = dlt;
@@ -115,6 +120,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   }
   f32x16 adq[NT];   // written first by the peeled first tile (zero C operand)
 
+  if constexpr (ROT) kst.rope(a.rope, 0, tid);
   kst.write(smem);
   vst.write(smem + TILE);
   vm_wait_all();   // Q / dO fragments resident before the loop (see vm_wait_all)
@@ -168,6 +174,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       }
     }
     if (t + 1 < nkt) {
+      if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);
       kst.write(nxt);
       vst.write(nxt + TILE);
     }
@@ -187,7 +194,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   if (active) {
     const int q0 = qb * BQ + w * 32;
     __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
-    wave_store_rows<DP>(adq, a.scale, smem + w * 32 * DP * 2, DQ, a.dqs[1], a.Nq - q0, a.D, lane);
+    wave_store_rows<DP, ROT ? -1 : 0>(adq, a.scale, smem + w * 32 * DP * 2, DQ, a.dqs[1], a.Nq - q0, a.D, lane,
+                                      &a.rope, q0);
   }
 }
 
@@ -196,7 +204,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
 // each 64-query Q / dO tile and its row constants (lse * log2 e, delta).  Per 32-query half:
 // S = Q K^T, dP = dO V^T (row reads), P = 2^(S sl2 - lse2), dS = P o (dP - delta),
 // dV^T += dO^T P and dK^T += Q^T dS (transposed reads of the dO / Q images).
-template <int DP, int NW, int MINW>
+template <int DP, int NW, int MINW, bool ROT = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -257,6 +265,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
       kf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, ok ? ko + d0 * 2 : 0x80000000u, 0, 0));
       vf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, ok ? vo + d0 * 2 : 0x80000000u, 0, 0));
     }
+    if constexpr (ROT) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) kf[s] = rope8<1>(kf[s], a.rope, key, 16 * s + 8 * h);
+    }
   }
   const float sl2 = a.scale * kLog2e;
 
@@ -281,7 +293,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   bf16x8 one01;
 #pragma unroll
   for (int j = 0; j < 8; ++j) one01[j] = (__bf16)((h == 0 && j < 2) ? 1.f : 0.f);
-  auto put = [&](int r, char* buf) {
+  auto put = [&](int r, char* buf, int qt) {
+    if constexpr (ROT) qst[r].rope(a.rope, 64 * qt, tid);
     qst[r].write(buf);
     gst[r].write(buf + TILE);
     if (tid < 64) {
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
       reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d[r];
     }
   };
-  put(0, smem);
+  put(0, smem, 0);
   vm_wait_all();   // K / V fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   auto step = [&](int qt, auto bsel_c, auto first_c, auto compute_c) {
@@ -358,7 +371,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
         }
       }
     }
-    if (qt + 1 < nqt) put(bsel ^ 1, nxt);
+    if (qt + 1 < nqt) put(bsel ^ 1, nxt, qt + 1);
     __syncthreads();
   };
   auto sweep = [&](auto compute_c) {
@@ -377,7 +390,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     char* scr = smem + w * 32 * DP * 2;
     __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)k0 * a.dks[1];
     __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)k0 * a.dvs[1];
-    wave_store_rows<DP>(adk, a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane);
+    wave_store_rows<DP, ROT ? -1 : 0>(adk, a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane, &a.rope, k0);
     wave_store_rows<DP>(adv, 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
   }
   (void)key;

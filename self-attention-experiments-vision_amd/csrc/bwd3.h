@@ -73,6 +73,7 @@ template <int DP, int NW> struct B3Stage {
   bool has;
   uint4 q, g, o;
   float lse2;
+  int qt_;               // query tile held in the registers (rotary position base)
 
   __device__ __forceinline__ void init(int tid, const AttnArgs& a) {
     row = tid / C::CPR;
@@ -87,6 +88,7 @@ template <int DP, int NW> struct B3Stage {
   __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rg,
                                        __amdgpu_buffer_rsrc_t ro, const AttnArgs& a, int qt, size_t rowoff,
                                        int tid) {
+    qt_ = qt;
     q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                       rq, oq + (unsigned)(qt * 32 * a.qs[1] * 2), 0, 0));
     g = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -98,7 +100,8 @@ template <int DP, int NW> struct B3Stage {
       lse2 = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
     }
   }
-  __device__ __forceinline__ void write(char* buf, int tid) const {
+  template <bool ROT = false>
+  __device__ __forceinline__ void write(char* buf, int tid, const RopeTab* rope = nullptr) const {
     const bf16x8 gv = __builtin_bit_cast(bf16x8, g), ov = __builtin_bit_cast(bf16x8, o);
     float part = 0.f;
 #pragma unroll
@@ -108,7 +111,10 @@ template <int DP, int NW> struct B3Stage {
     part += dpp_mov<0x4E>(part);
     if constexpr (C::CPR == 8) part += dpp_mov<0x141>(part);
     if (has) {
-      *reinterpret_cast<uint4*>(buf + loff) = q;
+      if constexpr (ROT)
+        *reinterpret_cast<uint4*>(buf + loff) = rope8<1>(q, *rope, qt_ * 32 + row, 8 * col);
+      else
+        *reinterpret_cast<uint4*>(buf + loff) = q;
       *reinterpret_cast<uint4*>(buf + C::QIMG + loff) = g;
       if (col == 0) reinterpret_cast<float*>(buf + 2 * C::QIMG + 128)[row] = -part;
     }
@@ -119,7 +125,9 @@ template <int DP, int NW> struct B3Stage {
 // NW waves x KPW sub-blocks of 32 keys per workgroup.  KPW = 2 (four waves, one per SIMD, the
 // whole register file each): the two sub-blocks of a wave share every Q / dO operand read and give
 // the scheduler two independent MFMA / exp chains; KPW = 1 (eight waves, two per SIMD).
-template <int DP, int NW, int KPW>
+// ROT: q / k rotated as they are staged (the K fragments also feed the K image, so dQ uses the
+// rotated K as it must), dq / dk rotated back as they are stored.
+template <int DP, int NW, int KPW, bool ROT = false>
 __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void attn_bwd3_kernel(AttnArgs a) {
   using C = B3<DP, NW, KPW>;
   constexpr int NS = C::NS, NT = C::NT, BK = C::BK, TB = C::TB, KS = C::KS;
@@ -168,6 +176,10 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
         kf[j][s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, ok ? ko + d0 * 2 : 0x80000000u, 0, 0));
         vf[j][s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, ok ? vo + d0 * 2 : 0x80000000u, 0, 0));
       }
+      if constexpr (ROT) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) kf[j][s] = rope8<1>(kf[j][s], a.rope, key, 16 * s + 8 * h);
+      }
     }
   }
 #pragma unroll
@@ -177,7 +189,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       const int rr = wrow + 32 * j + r32;
       *reinterpret_cast<bf16x8*>(dsb + rr * DP * 2 + 16 * ((2 * s + h) ^ swz<DP>(rr))) = kf[j][s];
     }
-  st.write(smem, tid);
+  st.template write<ROT>(smem, tid, &a.rope);
   vm_wait_all();
   __syncthreads();
 
@@ -270,8 +282,13 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       const int d0 = 16 * db + 4 * gq;
       if (qq < a.Nq && d0 < a.D) {
         typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-        const bf16x4 v = {(__bf16)(acc[0] * a.scale), (__bf16)(acc[1] * a.scale), (__bf16)(acc[2] * a.scale),
-                          (__bf16)(acc[3] * a.scale)};
+        bf16x4 v = {(__bf16)(acc[0] * a.scale), (__bf16)(acc[1] * a.scale), (__bf16)(acc[2] * a.scale),
+                    (__bf16)(acc[3] * a.scale)};
+        if constexpr (ROT) {   // back by -theta from the bf16 values (as the standalone pass would)
+          float x[4] = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+          rope_pairs<2, -1>(x, a.rope, qq, d0 / 2);
+          v = bf16x4{(__bf16)x[0], (__bf16)x[1], (__bf16)x[2], (__bf16)x[3]};
+        }
         __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)qq * a.dqs[1];
         *reinterpret_cast<bf16x4*>(DQ + d0) = v;
       }
@@ -362,7 +379,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       }
     }
     if (qt > 0) dq_tile(dsb + (bsel ^ 1) * C::DSIMG, qt - 1);
-    if (qt + 1 < nqt) st.write(smem + (bsel ^ 1) * TB, tid);
+    if (qt + 1 < nqt) st.template write<ROT>(smem + (bsel ^ 1) * TB, tid, &a.rope);
     __syncthreads();
   };
   {
@@ -383,7 +400,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       char* scr = smem + w * 32 * DP * 2;
       __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)k0 * a.dks[1];
       __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)k0 * a.dvs[1];
-      wave_store_rows<DP>(adk[j], a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane);
+      wave_store_rows<DP, ROT ? -1 : 0>(adk[j], a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane, &a.rope, k0);
       wave_store_rows<DP>(adv[j], 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
     }
   }

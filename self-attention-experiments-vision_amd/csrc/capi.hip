@@ -162,13 +162,13 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 };
 
 // lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
-template <int DP, int NW, int MINW, bool LSUM> int fwd2_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false> int fwd2_run(hipStream_t st, const AttnArgs& a) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   const long long grid = (long long)nqb * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
   const size_t lds = 4 * (size_t)F2<DP>::TILE;
-  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
   return check_launch("attn_fwd2");
 }
 
@@ -185,9 +185,9 @@ int dev_knob(const char* name) {
 constexpr int dev_knob(const char*) { return 0; }
 #endif
 
-template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
+template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
 #ifdef SAE_DEV_KNOBS
-  switch (var) {
+  if (!ROT) switch (var) {
     case 2: return fwd2_run<DP, 8, 2, true>(st, a);
     case 4: return fwd2_run<DP, 4, 2, true>(st, a);
     case 5: return fwd2_run<DP, 4, 3, true>(st, a);
@@ -199,45 +199,45 @@ template <int DP> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) 
   // N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt); at
   // D = 128 it is 2x slower
   if constexpr (DP <= 64)
-    if (a.Nk >= 512) return fwd2_run<DP, 4, 3, false>(st, a);
+    if (a.Nk >= 512) return fwd2_run<DP, 4, 3, false, ROT>(st, a);
   (void)var;
-  return fwd2_run<DP, 4, 2, true>(st, a);
+  return fwd2_run<DP, 4, 2, true, ROT>(st, a);
 }
 
 // lean bf16 backward (bwd2.h): dQ pass (publishes delta) then dK/dV pass
-template <int DP, int NWQ, int MQ, int NWK, int MK> int bwd2_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NWQ, int MQ, int NWK, int MK, bool ROT = false> int bwd2_run(hipStream_t st, const AttnArgs& a) {
   {
     const long long grid = (long long)((a.Nq + 32 * NWQ - 1) / (32 * NWQ)) * a.H * a.B;
     if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
     const size_t lds = 4 * (size_t)F2<DP>::TILE;
-    if (int rc = lds_attr((const void*)attn_bwd2_dq_kernel<DP, NWQ, MQ>, lds)) return rc;
-    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, NWQ, MQ>), dim3((unsigned)grid), dim3(64 * NWQ), lds, st, a);
+    if (int rc = lds_attr((const void*)attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT>, lds)) return rc;
+    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT>), dim3((unsigned)grid), dim3(64 * NWQ), lds, st, a);
     if (int rc = check_launch("attn_bwd2_dq")) return rc;
   }
   const long long grid = (long long)((a.Nk + 32 * NWK - 1) / (32 * NWK)) * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
   const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512);
-  if (int rc = lds_attr((const void*)attn_bwd2_dkdv_kernel<DP, NWK, MK>, lds)) return rc;
-  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, NWK, MK>), dim3((unsigned)grid), dim3(64 * NWK), lds, st, a);
+  if (int rc = lds_attr((const void*)attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT>, lds)) return rc;
+  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT>), dim3((unsigned)grid), dim3(64 * NWK), lds, st, a);
   return check_launch("attn_bwd2_dkdv");
 }
 
-template <int DP> int bwd2_run_default(hipStream_t st, const AttnArgs& a) {
-  return bwd2_run<DP, 4, 2, 4, 2>(st, a);
+template <int DP, bool ROT = false> int bwd2_run_default(hipStream_t st, const AttnArgs& a) {
+  return bwd2_run<DP, 4, 2, 4, 2, ROT>(st, a);
 }
 
 // single-pass bf16 backward (bwd3.h): one workgroup per (batch, head) holding all Nk <= 256 keys
 // (8 waves x 32 keys, two waves per SIMD); longer key ranges take the two-pass bwd2
 constexpr int kB3Keys = 256;
 
-template <int DP, int NW, int KPW> int bwd3_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NW, int KPW, bool ROT = false> int bwd3_run(hipStream_t st, const AttnArgs& a) {
   using C = B3<DP, NW, KPW>;
   static_assert(C::BK == kB3Keys, "bwd3 dispatch assumes 256-key blocks");
   const long long grid = (long long)a.H * a.B;
   if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3: %d keys > %d", a.Nk, C::BK);
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW>, C::LDS)) return rc;
-  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
+  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT>, C::LDS)) return rc;
+  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
   return check_launch("attn_bwd3");
 }
 
@@ -325,41 +325,44 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
 }
 
 // bf16 with the head mixes on the MFMA (th2.h); NWMAX = 8 or 16 waves per workgroup
-template <int DP, int NWMAX> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
+template <int DP, int NWMAX, bool ROT> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32;
   const size_t lds = th2_lds_bytes<DP>(a.H);
-  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX>, lds)) return rc;
-  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT>, lds)) return rc;
+  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
   return check_launch("th2_fwd");
 }
 
-template <int DP, int NWMAX> int th2_bwd_run(hipStream_t st, ThArgs a) {
+template <int DP, int NWMAX, bool ROT> int th2_bwd_run(hipStream_t st, ThArgs a) {
   const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32;
   a.nblk = nqb * a.B;
   const size_t lds = th2_lds_bytes<DP>(a.H), lds_kv = th2_kv_lds_bytes<DP>(a.H, NWMAX <= 8);
-  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX>, lds)) return rc;
-  if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX>, lds_kv)) return rc;
-  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT>, lds)) return rc;
+  if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT>, lds_kv)) return rc;
+  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
   if (int rc = check_launch("th2_bwd_q")) return rc;
-  hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
+  hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX, ROT>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
   if (int rc = check_launch("th2_bwd_kv")) return rc;
   hipLaunchKernelGGL(th_reduce_kernel, dim3(2 * a.H * a.H), dim3(256), 0, st, a);
   return check_launch("th_reduce");
 }
 
 template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
-  return a.H <= 8 ? th2_fwd_run<DP, 8>(st, a) : th2_fwd_run<DP, 16>(st, a);
+  if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true>(st, a) : th2_fwd_run<DP, 16, true>(st, a);
+  return a.H <= 8 ? th2_fwd_run<DP, 8, false>(st, a) : th2_fwd_run<DP, 16, false>(st, a);
 }
 template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
-  return a.H <= 8 ? th2_bwd_run<DP, 8>(st, a) : th2_bwd_run<DP, 16>(st, a);
+  if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true>(st, a) : th2_bwd_run<DP, 16, true>(st, a);
+  return a.H <= 8 ? th2_bwd_run<DP, 8, false>(st, a) : th2_bwd_run<DP, 16, false>(st, a);
 }
 
 }  // namespace
 
 int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
-           const float* th2, void* o, float* lse) {
+           const float* th2, void* o, float* lse, const RopeTab* rope) {
   ThArgs a;
   fill_th(a, d);
+  if (rope) a.rope = *rope;
   a.q = q;
   a.k = k;
   a.v = v;
@@ -374,6 +377,7 @@ int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
     if (dp == 32) return th2_fwd_dispatch<32>(st, a);
     if (dp == 64) return th2_fwd_dispatch<64>(st, a);
   }
+  if (rope) return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 talking-heads path (aligned strides)");
   if (d->heads > kThMaxH) return fail(SAE_EUNSUPPORTED, "talking heads: %d heads > %d on the fp32 / unaligned path",
                                       d->heads, kThMaxH);
 #define TH_F(T, DPV) \
@@ -395,9 +399,10 @@ size_t th_bwd_workspace_bytes(const sae_attn_desc* d) {
 
 int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
            const float* th2, const float* lse, const void* dout, void* dq, void* dk, void* dv, float* dth1,
-           float* dth2, void* workspace) {
+           float* dth2, void* workspace, const RopeTab* rope) {
   ThArgs a;
   fill_th(a, d);
+  if (rope) a.rope = *rope;
   a.q = q;
   a.k = k;
   a.v = v;
@@ -420,6 +425,7 @@ int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
     if (dp == 32) return th2_bwd_dispatch<32>(st, a);
     if (dp == 64) return th2_bwd_dispatch<64>(st, a);
   }
+  if (rope) return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 talking-heads path (aligned strides)");
   if (d->heads > kThMaxH) return fail(SAE_EUNSUPPORTED, "talking heads: %d heads > %d on the fp32 / unaligned path",
                                       d->heads, kThMaxH);
 #define TH_B(T, DPV) \
@@ -454,8 +460,40 @@ void sae_attn_desc_init(sae_attn_desc* d, int32_t batch, int32_t heads, int32_t 
   }
 }
 
+// rotary tables of the _rotary entry points: fp32 [max(seq_q, seq_k)][head_dim / 2]
+static int rope_check(const sae_attn_desc* d, const float* sin_tab, const float* cos_tab) {
+  if (!sin_tab || !cos_tab) return fail(SAE_EINVAL, "rotary: sin_tab / cos_tab must be non-NULL");
+  if (!aligned16(sin_tab) || !aligned16(cos_tab)) return fail(SAE_EINVAL, "rotary: tables must be 16-byte aligned");
+  if (d->head_dim % 8) return fail(SAE_EUNSUPPORTED, "rotary: fused rotary needs head_dim %% 8 == 0 (got %d)", d->head_dim);
+  return SAE_OK;
+}
+static RopeTab make_rope(const sae_attn_desc* d, const float* sin_tab, const float* cos_tab) {
+  RopeTab t;
+  t.sin = sin_tab;
+  t.cos = cos_tab;
+  t.P = d->head_dim / 2;
+  t.n = std::max(d->seq_q, d->seq_k);
+  return t;
+}
+
+static int attn_fwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                         const float* bias_h, const float* bias_w, void* o, float* lse, const RopeTab* rope);
+
 int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
                  const float* bias_h, const float* bias_w, void* o, float* lse) {
+  return attn_fwd_impl(stream, d, q, k, v, bias_h, bias_w, o, lse, nullptr);
+}
+
+int sae_attn_fwd_rotary(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                        const float* sin_tab, const float* cos_tab, void* o, float* lse) {
+  if (!d) return fail(SAE_EINVAL, "NULL descriptor");
+  if (int rc = rope_check(d, sin_tab, cos_tab)) return rc;
+  const RopeTab t = make_rope(d, sin_tab, cos_tab);
+  return attn_fwd_impl(stream, d, q, k, v, nullptr, nullptr, o, lse, &t);
+}
+
+static int attn_fwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                         const float* bias_h, const float* bias_w, void* o, float* lse, const RopeTab* rope) {
   int rc = validate(d, false);
   if (rc) return rc;
   if (!q || !k || !v || !o) return fail(SAE_EINVAL, "q/k/v/o must be non-NULL");
@@ -475,6 +513,15 @@ int sae_attn_fwd(void* stream, const sae_attn_desc* d, const void* q, const void
                    strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o);
   const int var = dev_knob("SAE_FWD_VARIANT");
+  if (rope) {   // rotary rides on the lean bf16 kernels only
+    if (d->dtype != SAE_DTYPE_BF16 || !vec || rel || d->flags)
+      return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 path (16-byte aligned strides, no flags)");
+    a.rope = *rope;
+    const int dp = pick_dp(d->head_dim);
+    if (dp == 32) return fwd2_dispatch<32, true>((hipStream_t)stream, a, 0);
+    if (dp == 64) return fwd2_dispatch<64, true>((hipStream_t)stream, a, 0);
+    return fwd2_dispatch<128, true>((hipStream_t)stream, a, 0);
+  }
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     if (dp == 32) return fwd2_dispatch<32>((hipStream_t)stream, a, var);
@@ -493,9 +540,32 @@ size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
   return delta_bytes(d);
 }
 
+static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                         const void* o, const float* lse, const void* dout, const float* bias_h,
+                         const float* bias_w, void* dq, void* dk, void* dv, float* dbias_h, float* dbias_w,
+                         void* workspace, const RopeTab* rope);
+
 int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
                  const void* o, const float* lse, const void* dout, const float* bias_h, const float* bias_w,
                  void* dq, void* dk, void* dv, float* dbias_h, float* dbias_w, void* workspace) {
+  return attn_bwd_impl(stream, d, q, k, v, o, lse, dout, bias_h, bias_w, dq, dk, dv, dbias_h, dbias_w, workspace,
+                       nullptr);
+}
+
+int sae_attn_bwd_rotary(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                        const void* o, const float* lse, const void* dout, const float* sin_tab,
+                        const float* cos_tab, void* dq, void* dk, void* dv, void* workspace) {
+  if (!d) return fail(SAE_EINVAL, "NULL descriptor");
+  if (int rc = rope_check(d, sin_tab, cos_tab)) return rc;
+  const RopeTab t = make_rope(d, sin_tab, cos_tab);
+  return attn_bwd_impl(stream, d, q, k, v, o, lse, dout, nullptr, nullptr, dq, dk, dv, nullptr, nullptr, workspace,
+                       &t);
+}
+
+static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                         const void* o, const float* lse, const void* dout, const float* bias_h,
+                         const float* bias_w, void* dq, void* dk, void* dv, float* dbias_h, float* dbias_w,
+                         void* workspace, const RopeTab* rope) {
   int rc = validate(d, true);
   if (rc) return rc;
   if (!q || !k || !v || !o || !lse || !dout || !dq || !dk || !dv || !workspace)
@@ -527,6 +597,16 @@ int sae_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const void
                    aligned16(k) && aligned16(v) && aligned16(o) && aligned16(dout) && aligned16(dq) &&
                    aligned16(dk) && aligned16(dv);
   const int var = dev_knob("SAE_BWD_VARIANT");
+  if (rope) {   // rotary rides on the lean bf16 kernels only
+    const int dp = pick_dp(d->head_dim);
+    if (d->dtype != SAE_DTYPE_BF16 || !vec || rel || d->flags || dp > 64)
+      return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 path with head_dim <= 64 (16-byte aligned "
+                  "strides, no flags)");
+    a.rope = *rope;
+    hipStream_t st = (hipStream_t)stream;
+    if (a.Nk <= kB3Keys) return dp == 32 ? bwd3_run<32, 8, 1, true>(st, a) : bwd3_run<64, 8, 1, true>(st, a);
+    return dp == 32 ? bwd2_run_default<32, true>(st, a) : bwd2_run_default<64, true>(st, a);
+  }
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;
@@ -696,6 +776,40 @@ int sae_th_attn_bwd(void* stream, const sae_attn_desc* d, const void* q, const v
     return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
                 SAE_TH_MAX_HEAD_DIM);
   if (int rc = th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace)) return rc;
+  return ok();
+}
+
+int sae_th_attn_fwd_rotary(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                           const float* th1, const float* th2, const float* sin_tab, const float* cos_tab, void* o,
+                           float* lse) {
+  int rc = validate(d, false);
+  if (rc) return rc;
+  if (d->flags) return fail(SAE_EINVAL, "talking heads takes no flags");
+  if (!q || !k || !v || !th1 || !th2 || !o || !lse) return fail(SAE_EINVAL, "NULL argument");
+  if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
+    return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
+                SAE_TH_MAX_HEAD_DIM);
+  if (int rc2 = rope_check(d, sin_tab, cos_tab)) return rc2;
+  const RopeTab t = make_rope(d, sin_tab, cos_tab);
+  if (int rc2 = th_fwd(stream, d, q, k, v, th1, th2, o, lse, &t)) return rc2;
+  return ok();
+}
+
+int sae_th_attn_bwd_rotary(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
+                           const float* th1, const float* th2, const float* lse, const void* dout,
+                           const float* sin_tab, const float* cos_tab, void* dq, void* dk, void* dv, float* dth1,
+                           float* dth2, void* workspace) {
+  int rc = validate(d, true);
+  if (rc) return rc;
+  if (d->flags) return fail(SAE_EINVAL, "talking heads takes no flags");
+  if (!q || !k || !v || !th1 || !th2 || !lse || !dout || !dq || !dk || !dv || !dth1 || !dth2 || !workspace)
+    return fail(SAE_EINVAL, "NULL argument");
+  if (d->heads > SAE_TH_MAX_HEADS || d->head_dim > SAE_TH_MAX_HEAD_DIM)
+    return fail(SAE_EUNSUPPORTED, "talking heads needs heads <= %d and head_dim <= %d", SAE_TH_MAX_HEADS,
+                SAE_TH_MAX_HEAD_DIM);
+  if (int rc2 = rope_check(d, sin_tab, cos_tab)) return rc2;
+  const RopeTab t = make_rope(d, sin_tab, cos_tab);
+  if (int rc2 = th_bwd(stream, d, q, k, v, th1, th2, lse, dout, dq, dk, dv, dth1, dth2, workspace, &t)) return rc2;
   return ok();
 }
 

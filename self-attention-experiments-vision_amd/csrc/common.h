@@ -248,6 +248,64 @@ __device__ __forceinline__ void store4(T* rowp, int d0, int D, float a, float b,
   }
 }
 
+// ------------------------------------------------------------------------------- rotary
+// GPT-J interleaved rotary (models/layers/position_embed.py:8-20) applied while q / k are staged
+// and undone on dq / dk as they are stored (the attention kernels' ROT instances): pairs
+// (2i, 2i+1) of the head dim at position pos, fp32 tables sin / cos [n][P = D / 2]:
+//   y[2i] = x[2i] cos - x[2i+1] sin,  y[2i+1] = x[2i+1] cos + x[2i] sin   (SGN = -1: by -theta)
+// with explicit FMAs, so the fused path and the standalone rotary_kernel round identically.
+struct RopeTab {
+  const float* sin;
+  const float* cos;
+  int P, n;
+};
+template <int NP, int SGN>
+__device__ __forceinline__ void rope_pairs(float* x, const RopeTab& t, int pos, int i0) {
+  const float* sp = t.sin + (long long)pos * t.P + i0;
+  const float* cp = t.cos + (long long)pos * t.P + i0;
+  float sv[NP], cv[NP];
+  if constexpr (NP == 4) {
+    const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp), c4 = *reinterpret_cast<const f32x4*>(cp);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sv[j] = s4[j];
+      cv[j] = c4[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      sv[j] = sp[j];
+      cv[j] = cp[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const float sn = SGN > 0 ? sv[j] : -sv[j];
+    const float x0 = x[2 * j], x1 = x[2 * j + 1];
+    x[2 * j] = __builtin_fmaf(x0, cv[j], -(x1 * sn));
+    x[2 * j + 1] = __builtin_fmaf(x1, cv[j], x0 * sn);
+  }
+}
+// one 16-byte chunk = head-dim elements d0 .. d0 + 7 (d0 % 8 == 0) of position pos; chunks past the
+// head dim (zero padding) or past the table pass through
+template <int SGN>
+__device__ __forceinline__ uint4 rope8(uint4 v, const RopeTab& t, int pos, int d0) {
+  if (pos >= t.n || d0 >= 2 * t.P) return v;
+  const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (float)b[j];
+  rope_pairs<4, SGN>(x, t, pos, d0 / 2);
+  bf16x8 y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = (__bf16)x[j];
+  return __builtin_bit_cast(uint4, y);
+}
+template <int SGN>
+__device__ __forceinline__ bf16x8 rope8(bf16x8 v, const RopeTab& t, int pos, int d0) {
+  return __builtin_bit_cast(bf16x8, rope8<SGN>(__builtin_bit_cast(uint4, v), t, pos, d0));
+}
+
 // ------------------------------------------------------------------------ epilogue stores
 // A wave's 32 output rows held as NT accumulator tiles acc[t] = X^T (accumulator row = head-dim
 // column 32t + row_of(r, h), accumulator column = the wave's output row lane & 31), scaled by sc,
@@ -257,9 +315,12 @@ __device__ __forceinline__ void store4(T* rowp, int d0, int D, float a, float b,
 // 16 B slivers of 32 rows, so no partial cache lines are written at the row stride
 // (MI355X_MICROARCH.md "attention epilogue store tail").  Rows >= nrows and columns >= D are not
 // stored.  Wave-local: the scratch must not be in use by other waves.
-template <int DP>
+// RSGN != 0: the rows are positions pos0 .. pos0 + 31 and each chunk is rotated by RSGN theta
+// (rope8) on its way out (dq / dk of the rotary instances: the gradient of the un-rotated input).
+template <int DP, int RSGN = 0>
 __device__ __forceinline__ void wave_store_rows(const f32x16* acc, float sc, char* scratch, __bf16* dst,
-                                                long long rs, int nrows, int D, int lane) {
+                                                long long rs, int nrows, int D, int lane,
+                                                const RopeTab* rope = nullptr, int pos0 = 0) {
   constexpr int NT = DP / 32, CPR = DP / 8, RPI = 64 / CPR;
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
   const int h = lane >> 5, r = lane & 31;
@@ -276,7 +337,10 @@ __device__ __forceinline__ void wave_store_rows(const f32x16* acc, float sc, cha
 #pragma unroll
   for (int it = 0; it < 32 / RPI; ++it) {
     const int rr = it * RPI + lane / CPR;
-    const uint4 v = *reinterpret_cast<const uint4*>(scratch + rr * DP * 2 + 16 * (c ^ swz<DP>(rr)));
+    uint4 v = *reinterpret_cast<const uint4*>(scratch + rr * DP * 2 + 16 * (c ^ swz<DP>(rr)));
+    if constexpr (RSGN != 0) {
+      if (rr < nrows) v = rope8<RSGN>(v, *rope, pos0 + rr, c * 8);
+    }
     if (rr < nrows && c * 8 < D) *reinterpret_cast<uint4*>(dst + (long long)rr * rs + c * 8) = v;
   }
   __builtin_amdgcn_wave_barrier();

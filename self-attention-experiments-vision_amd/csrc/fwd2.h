@@ -68,6 +68,14 @@ struct F2Stage {
       if (64 * F2<DP>::CPR % (64 * NW) == 0 || loff[i] != 0xffffffffu)
         *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
   }
+  // rotary on the staged chunks (rows = positions pos0 .. pos0 + 63), before write()
+  __device__ __forceinline__ void rope(const RopeTab& t, int pos0, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = tid + 64 * NW * i;
+      if (id < 64 * F2<DP>::CPR) v[i] = rope8<1>(v[i], t, pos0 + id / F2<DP>::CPR, 8 * (id % F2<DP>::CPR));
+    }
+  }
 };
 
 template <int DP, int NW, bool LSUM, bool FIRST>
@@ -178,7 +186,9 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
   }
 }
 
-template <int DP, int NW, int MINW, bool LSUM>
+// ROT: q and k are rotated (rotary, common.h rope8) as they are staged -- q fragments once, each
+// K tile as it goes to LDS -- so the rotated tensors never exist in HBM.
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -221,6 +231,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       const unsigned off = (16 * s + 8 * h < a.D) ? qo + (16 * s + 8 * h) * 2 : 0x80000000u;
       qf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0));
     }
+    if constexpr (ROT) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
+    }
   }
   // per-lane LDS read addresses: K rows r32 (+32 as an immediate), V^T transposed reads
   unsigned ka[NS], va[2 * NT];
@@ -242,6 +256,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   float m = -kInf, l = 0.f;
   const float sl2 = a.scale * kLog2e;
 
+  if constexpr (ROT) kst.rope(a.rope, 0, tid);
   kst.write(smem);
   vst.write(smem + TILE);
   vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
@@ -261,6 +276,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       fwd2_tile<DP, NW, LSUM, decltype(first_c)::value>(cur, cur + TILE, qf, acco, lacc, m, l,
                                                         min(64, a.Nk - 64 * t), sl2, ka, va, h);
     if (t + 1 < nkt) {
+      if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);
       kst.write(nxt);
       vst.write(nxt + TILE);
     }

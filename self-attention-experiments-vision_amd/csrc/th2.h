@@ -159,7 +159,7 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
 }
 
 // ================================================================================= forward
-template <int DP, int NWMAX>
+template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
@@ -180,9 +180,13 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
 
   th2_zero_pad(XS, H, tid, 64 * H);
   th2_zero_pad(XP, H, tid, 64 * H);
+  constexpr bool rot = ROT;   // rotary: q / k rotated as they are loaded
   bf16x8 qf[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
+  }
   const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);   // S1 = T1^T S
   const Th2Mix m2 = th2_mix<false, true>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
   const int nkt = (a.Nk + 31) / 32;
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   auto scores = [&](int kt) {
     bf16x8 kc[NS];
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) kc[s_] = kn[s_];
+    for (int s_ = 0; s_ < NS; ++s_) kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
     load_k(kt + 1 < nkt ? kt + 1 : 0);
     f32x16 s = zero16();
 #pragma unroll
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
 // ============================================================================ bwd: query
 // pass A: delta_i = rowsum(P_i o dP_i), dP = T2 dP2, dP2_j = dO_j V_j^T; dT2 = sum P (x) dP2.
 // pass B: dS1 = P o (dP - delta), dT1 = sum S (x) dS1, dS = T1 dS1, dQ_w += scale dS_w K_w.
-template <int DP, int NWMAX>
+template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
@@ -324,10 +328,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 
   th2_zero_pad(XS, H, tid, 64 * H);
   th2_zero_pad(XG, H, tid, 64 * H);
+  constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dq rotated back
   bf16x8 qf[NS], gf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
     gf[s] = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s, h);
   }
   const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);    // S1 = T1^T S        (image)
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     bf16x8 kc[NS], vc[NS];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
-      kc[s_] = kn[s_];
+      kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
       vc[s_] = vn[s_];
     }
     load_kv(kt + 1 < nkt ? kt + 1 : 0);
@@ -419,6 +425,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   for (int kt = 0; kt < nkt; ++kt) {
     kst.load(K, kt * 32, a.Nk, a.ks[1], a.D, lane);
     tiles(kt);
+    if (rot) kst.rope(a.rope, kt * 32, lane);
     kst.write(ldsK, lane);
     __syncthreads();
     for (int blk = w; blk < 32; blk += H) {
@@ -453,9 +460,14 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        store4<__bf16, true>(DQ, 32 * t + 8 * g4 + 4 * h, a.D, adq[t][4 * g4] * sc, adq[t][4 * g4 + 1] * sc,
-                             adq[t][4 * g4 + 2] * sc, adq[t][4 * g4 + 3] * sc);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * t + 8 * g4 + 4 * h;
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = (float)(__bf16)(adq[t][4 * g4 + e] * sc);
+        if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, q, d0 / 2);
+        store4<__bf16, true>(DQ, d0, a.D, x[0], x[1], x[2], x[3]);
+      }
   }
 }
 
@@ -464,7 +476,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 // (same mixes), dV_w^T += dO_w^T P2_w, dK_w^T += scale Q_w^T dS_w.  The score tiles keep the key
 // on the accumulator rows and the query on the lane, so image position = key * 32 + query and the
 // per-head operands read query runs of a key: plain 16-byte row reads.
-template <int DP, int NWMAX>
+template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
@@ -487,10 +499,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 
   th2_zero_pad(XS, H, tid, 64 * H);
   th2_zero_pad(XG, H, tid, 64 * H);
+  constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dk rotated back
   bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     kf[s] = gfrag<__bf16, true>(K, key, a.Nk, a.ks[1], a.D, s, h);
+    if (rot) kf[s] = rope8<1>(kf[s], a.rope, key, 16 * s + 8 * h);
     vf[s] = gfrag<__bf16, true>(V, key, a.Nk, a.vs[1], a.D, s, h);
   }
   if (w == 0) {
@@ -517,6 +531,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   if constexpr (TWO) {
     gst.load(G, 0, a.Nq, a.dos[1], a.D, lane);
     qst.load(Q, 0, a.Nq, a.qs[1], a.D, lane);
+    if (rot) qst.rope(a.rope, 0, lane);
     gst.write(buf, lane);
     qst.write(bufQ, lane);
   }
@@ -549,6 +564,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
           ga = I::rowfrag(buf, r32, s_, h);
         } else {
           qa = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s_, h);
+          if (rot) qa = rope8<1>(qa, a.rope, q, 16 * s_ + 8 * h);
           ga = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s_, h);
         }
         s = MF<__bf16>::mma(kf[s_], qa, s);
@@ -590,7 +606,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) adv[t] = MF<__bf16>::mma(I::colfrag(buf, 0, s2, 32 * t, lane), pf, adv[t]);
     }
-    if constexpr (!TWO) qst.write(bufQ, lane);   // one buffer: Q after this wave's own dO reads
+    if constexpr (!TWO) {   // one buffer: Q after this wave's own dO reads
+      if (rot) qst.rope(a.rope, qt * 32, lane);
+      qst.write(bufQ, lane);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 sf = th2_rowB(XG, w, s2, lane);
@@ -599,6 +618,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     }
     if constexpr (TWO) {
       if (qt + 1 < nqt) {   // wave-private images: after this wave's own reads
+        if (rot) qst.rope(a.rope, (qt + 1) * 32, lane);
         gst.write(buf, lane);
         qst.write(bufQ, lane);
       }
@@ -614,8 +634,11 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d0 = 32 * t + 8 * g4 + 4 * h;
-        store4<__bf16, true>(DK, d0, a.D, adk[t][4 * g4] * sc, adk[t][4 * g4 + 1] * sc, adk[t][4 * g4 + 2] * sc,
-                             adk[t][4 * g4 + 3] * sc);
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = (float)(__bf16)(adk[t][4 * g4 + e] * sc);
+        if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, key, d0 / 2);
+        store4<__bf16, true>(DK, d0, a.D, x[0], x[1], x[2], x[3]);
         store4<__bf16, true>(DV, d0, a.D, adv[t][4 * g4], adv[t][4 * g4 + 1], adv[t][4 * g4 + 2], adv[t][4 * g4 + 3]);
       }
   }

@@ -42,6 +42,7 @@ struct ThArgs {
   int B, H, Nq, Nk, D, nblk;
   long long qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
   float scale;
+  RopeTab rope;     // rotary tables (th2 kernels rotate q / k when rope.sin != nullptr)
 };
 
 // ---- exchange buffer: one 32x32 fp32 accumulator per head, [reg>>2][lane][reg&3]
@@ -114,6 +115,14 @@ template <typename T, int DP, bool VEC> struct WStage {
       const int id = lane + 64 * i;
       const int r = id / CPR, c = id % CPR;
       *reinterpret_cast<uint4*>(lds + r * (DP * 2) + 16 * (c ^ swz<DP>(r))) = v[i];
+    }
+  }
+  // rotary on the staged rows row0 .. row0 + 31 (bf16), before write()
+  __device__ __forceinline__ void rope(const RopeTab& t, int row0, int lane) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = lane + 64 * i;
+      v[i] = rope8<1>(v[i], t, row0 + id / CPR, (id % CPR) * EPC);
     }
   }
 };
@@ -560,8 +569,8 @@ __global__ __launch_bounds__(256) void th_reduce_kernel(ThArgs a) {
 // ---------------------------------------------------------------- launchers (capi.hip)
 struct sae_attn_desc;
 int th_fwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
-           const float* th2, void* o, float* lse);
+           const float* th2, void* o, float* lse, const sae::RopeTab* rope = nullptr);
 size_t th_bwd_workspace_bytes(const sae_attn_desc* d);
 int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v, const float* th1,
            const float* th2, const float* lse, const void* dout, void* dq, void* dk, void* dv, float* dth1,
-           float* dth2, void* workspace);
+           float* dth2, void* workspace, const sae::RopeTab* rope = nullptr);

@@ -156,8 +156,9 @@ __global__ __launch_bounds__(256) void rotary_kernel(RotArgs a) {
   const float s = a.sgn * a.sin_t[(long long)n * P + i];
   const float c = a.cos_t[(long long)n * P + i];
   const float x0 = (float)xp[0], x1 = (float)xp[1];
-  yp[0] = (T)(x0 * c - x1 * s);
-  yp[1] = (T)(x1 * c + x0 * s);
+  // explicit FMAs, exactly as rope_pairs (common.h) in the fused kernels
+  yp[0] = (T)__builtin_fmaf(x0, c, -(x1 * s));
+  yp[1] = (T)__builtin_fmaf(x1, c, x0 * s);
 }
 
 }  // namespace sae

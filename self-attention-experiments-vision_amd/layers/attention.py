@@ -28,6 +28,9 @@ import torch.nn.functional as F
 
 from .. import ops
 
+# rotary base (position_embed.py: build-defined, survey D6); the standalone ops.rotary default
+ROTARY_BASE = 10000.0
+
 __all__ = ["DenseGeneral", "AttentionBlock", "SelfAttentionBlock", "TalkingHeadsBlock",
            "ClassSelfAttentionBlock", "LCSelfAttentionBlock", "lecun_normal_", "flax_params",
            "load_flax_params"]
@@ -151,18 +154,18 @@ class AttentionBlock(nn.Module):
             kv = ops.dense(xkv, [wk.reshape(C, HD), wv.reshape(C, HD)],
                            bias(self.keys, self.values) if bias else None, dt).view(B, Nk, 2, H, D)
             k, v = kv[:, :, 0], kv[:, :, 1]
-        if self.rotary:
-            q, k = ops.rotary(q), ops.rotary(k)
-        if self.talking_heads and self_attn and not self.rotary:
+        # rotary (position_embed.py:8-20) rides inside the attention kernels: q / k stay un-rotated
+        rope = ROTARY_BASE if self.rotary else None
+        if self.talking_heads and self_attn:
             o = ops.talking_heads_attention_packed(qkv, self.TalkingHeadsBlock_0.talking_heads_transform,
-                                                   self.TalkingHeadsBlock_1.talking_heads_transform, scale)
+                                                   self.TalkingHeadsBlock_1.talking_heads_transform, scale, rope)
         elif self.talking_heads:
             o = ops.talking_heads_attention(q, k, v, self.TalkingHeadsBlock_0.talking_heads_transform,
-                                            self.TalkingHeadsBlock_1.talking_heads_transform, scale)
-        elif self_attn and not self.rotary:
-            o = ops.attention_packed(qkv, scale)
+                                            self.TalkingHeadsBlock_1.talking_heads_transform, scale, rope)
+        elif self_attn:
+            o = ops.attention_packed(qkv, scale, rope)
         else:
-            o = ops.attention(q, k, v, scale)
+            o = ops.attention(q, k, v, scale, rotary=rope)
         wo = self.DenseGeneral_0.kernel.reshape(HD, self._out_ch_eff)
         y = ops.dense(o.reshape(B, Nq, HD), wo, self.DenseGeneral_0.bias if self.use_bias else None, dt)
         if self.out_dropout_rate > 0.0:

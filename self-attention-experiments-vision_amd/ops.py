@@ -117,21 +117,41 @@ def _make_desc(q, k, v, o, scale, dout=None, dq=None, dk=None, dv=None, grid=Non
     return d
 
 
-def _fwd(q, k, v, scale, bias_h=None, bias_w=None, grid=None):
+def _rope_tabs(q, k, rope):
+    """(sin, cos) fp32 [max(Nq, Nk), D / 2] for the fused-rotary entry points (``rope`` = base)."""
+    return rotary_tables(max(q.shape[1], k.shape[1]), q.shape[-1], q.device, rope)
+
+
+def rope_fused_ok(*ts: torch.Tensor) -> bool:
+    """Whether the fused-rotary kernels take these [B, N, H, D] tensors (sae_attn_*_rotary:
+    bf16, head_dim % 8 == 0 and <= 64, 16-byte aligned token / head strides)."""
+    t0 = ts[0]
+    D = t0.shape[-1]
+    return (t0.dtype == torch.bfloat16 and D % 8 == 0 and D <= 64 and
+            all(t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(2) % 8 == 0
+                and t.data_ptr() % 16 == 0 for t in ts))
+
+
+def _fwd(q, k, v, scale, bias_h=None, bias_w=None, grid=None, rope=None):
     lib = L.load()
     B, Nq, H, D = q.shape
     o = torch.empty((B, Nq, H, D), dtype=q.dtype, device=q.device)
     lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
     d = _make_desc(q, k, v, o, scale, grid=grid)
     tok = _TIMER.begin("attn_fwd") if _TIMER is not None else None
-    L.check(lib.sae_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(bias_h),
-                             _ptr(bias_w), _ptr(o), _ptr(lse)))
+    if rope is not None:   # q / k un-rotated: the kernels rotate them while staging
+        sin, cos = _rope_tabs(q, k, rope)
+        L.check(lib.sae_attn_fwd_rotary(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(sin),
+                                        _ptr(cos), _ptr(o), _ptr(lse)))
+    else:
+        L.check(lib.sae_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(bias_h),
+                                 _ptr(bias_w), _ptr(o), _ptr(lse)))
     if tok is not None:
         _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
     return o, lse
 
 
-def _bwd(q, k, v, o, lse, do, dq, dk, dv, scale, bias_h=None, bias_w=None, grid=None):
+def _bwd(q, k, v, o, lse, do, dq, dk, dv, scale, bias_h=None, bias_w=None, grid=None, rope=None):
     lib = L.load()
     d = _make_desc(q, k, v, o, scale, do, dq, dk, dv, grid=grid)
     ws = torch.empty(lib.sae_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
@@ -139,9 +159,14 @@ def _bwd(q, k, v, o, lse, do, dq, dk, dv, scale, bias_h=None, bias_w=None, grid=
     if grid is not None:
         dbh, dbw = torch.empty_like(bias_h), torch.empty_like(bias_w)
     tok = _TIMER.begin("attn_bwd") if _TIMER is not None else None
-    L.check(lib.sae_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse),
-                             _ptr(do), _ptr(bias_h), _ptr(bias_w), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dbh),
-                             _ptr(dbw), _ptr(ws)))
+    if rope is not None:   # dq / dk for the un-rotated q / k
+        sin, cos = _rope_tabs(q, k, rope)
+        L.check(lib.sae_attn_bwd_rotary(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse),
+                                        _ptr(do), _ptr(sin), _ptr(cos), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(ws)))
+    else:
+        L.check(lib.sae_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse),
+                                 _ptr(do), _ptr(bias_h), _ptr(bias_w), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dbh),
+                                 _ptr(dbw), _ptr(ws)))
     if tok is not None:
         _TIMER.end(tok, tuple(q.shape[:2]) + (k.shape[1],) + tuple(q.shape[2:]))
     return dbh, dbw
@@ -153,11 +178,11 @@ def _grad_in(g: torch.Tensor) -> torch.Tensor:
 
 class _Attention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale, bias_h, bias_w, grid):
+    def forward(ctx, q, k, v, scale, bias_h, bias_w, grid, rope):
         _require_gpu(q, k, v)
-        o, lse = _fwd(q, k, v, scale, bias_h, bias_w, grid)
+        o, lse = _fwd(q, k, v, scale, bias_h, bias_w, grid, rope)
         ctx.save_for_backward(q, k, v, o, lse, bias_h, bias_w)
-        ctx.scale, ctx.grid = scale, grid
+        ctx.scale, ctx.grid, ctx.rope = scale, grid, rope
         return o
 
     @staticmethod
@@ -167,18 +192,18 @@ class _Attention(torch.autograd.Function):
         dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
         dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
         dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
-        dbh, dbw = _bwd(q, k, v, o, lse, do, dq, dk, dv, ctx.scale, bias_h, bias_w, ctx.grid)
-        return dq, dk, dv, None, dbh, dbw, None
+        dbh, dbw = _bwd(q, k, v, o, lse, do, dq, dk, dv, ctx.scale, bias_h, bias_w, ctx.grid, ctx.rope)
+        return dq, dk, dv, None, dbh, dbw, None, None
 
 
 class _AttentionPacked(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, scale):
+    def forward(ctx, qkv, scale, rope):
         _require_gpu(qkv)
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        o, lse = _fwd(q, k, v, scale)
+        o, lse = _fwd(q, k, v, scale, rope=rope)
         ctx.save_for_backward(qkv, o, lse)
-        ctx.scale = scale
+        ctx.scale, ctx.rope = scale, rope
         return o
 
     @staticmethod
@@ -187,35 +212,47 @@ class _AttentionPacked(torch.autograd.Function):
         do = _grad_in(do)
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         _bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
-             ctx.scale)
-        return dqkv, None
+             ctx.scale, rope=ctx.rope)
+        return dqkv, None, None
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: Optional[float] = None,
-              bias: Optional[Tuple[torch.Tensor, torch.Tensor, Tuple[int, int]]] = None) -> torch.Tensor:
+              bias: Optional[Tuple[torch.Tensor, torch.Tensor, Tuple[int, int]]] = None,
+              rotary: Optional[float] = None) -> torch.Tensor:
     """softmax(scale * q k^T [+ relpos bias]) v on token-major [B, N, H, D] tensors.
 
     ``scale`` defaults to the reference's 1/sqrt(head_ch) (attention.py:39).  ``bias`` is
-    ``(bias_h, bias_w, (Hs, Ws))`` from :func:`relpos_bias` (BoTNet)."""
+    ``(bias_h, bias_w, (Hs, Ws))`` from :func:`relpos_bias` (BoTNet).  ``rotary`` (a base, e.g.
+    10000.0): q and k are rotated first (position_embed.py:8-20) -- inside the kernels' staging
+    where they take it (:func:`rope_fused_ok`), else by the standalone rotary pass."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
+    if rotary is not None and bias is None:
+        if rope_fused_ok(q, k, v):
+            return _Attention.apply(q, k, v, float(scale), None, None, None, float(rotary))
+        q, k = _Rotary.apply(q, float(rotary)), _Rotary.apply(k, float(rotary))
+    elif rotary is not None:
+        q, k = _Rotary.apply(q, float(rotary)), _Rotary.apply(k, float(rotary))
     if bias is None:
-        return _Attention.apply(q, k, v, float(scale), None, None, None)
+        return _Attention.apply(q, k, v, float(scale), None, None, None, None)
     bh, bw, grid = bias
-    return _Attention.apply(q, k, v, float(scale), bh, bw, tuple(grid))
+    return _Attention.apply(q, k, v, float(scale), bh, bw, tuple(grid), None)
 
 
-def attention_packed(qkv: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
-    """Self-attention on a packed projection ``qkv`` [B, N, 3, H, D] (one fused QKV GEMM output)."""
+def attention_packed(qkv: torch.Tensor, scale: Optional[float] = None, rotary: Optional[float] = None) -> torch.Tensor:
+    """Self-attention on a packed projection ``qkv`` [B, N, 3, H, D] (one fused QKV GEMM output);
+    ``rotary`` as in :func:`attention`."""
     if qkv.dim() != 5 or qkv.shape[2] != 3:
         raise ValueError(f"expected qkv [B, N, 3, H, D], got {tuple(qkv.shape)}")
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
-    return _AttentionPacked.apply(qkv, float(scale))
+    if rotary is not None and not rope_fused_ok(qkv[:, :, 0]):
+        return attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], scale, rotary=rotary)
+    return _AttentionPacked.apply(qkv, float(scale), None if rotary is None else float(rotary))
 
 
 # ----------------------------------------------------------------------------- talking heads
-def _th_fwd(q, k, v, th1, th2, scale):
+def _th_fwd(q, k, v, th1, th2, scale, rope=None):
     lib = L.load()
     B, Nq, H, D = q.shape
     th1c = th1.detach().to(torch.float32).contiguous()
@@ -224,22 +261,33 @@ def _th_fwd(q, k, v, th1, th2, scale):
     lse = torch.empty((B, H, Nq), dtype=torch.float32, device=q.device)
     d = _make_desc(q, k, v, o, scale)
     tok = _TIMER.begin("th_attn_fwd") if _TIMER is not None else None
-    L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
-                                _ptr(th2c), _ptr(o), _ptr(lse)))
+    if rope is not None:
+        sin, cos = _rope_tabs(q, k, rope)
+        L.check(lib.sae_th_attn_fwd_rotary(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
+                                           _ptr(th2c), _ptr(sin), _ptr(cos), _ptr(o), _ptr(lse)))
+    else:
+        L.check(lib.sae_th_attn_fwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1c),
+                                    _ptr(th2c), _ptr(o), _ptr(lse)))
     if tok is not None:
         _TIMER.end(tok, (B, Nq, k.shape[1], H, D))
     return o, lse, th1c, th2c
 
 
-def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale):
+def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale, rope=None):
     lib = L.load()
     dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
     d = _make_desc(q, k, v, None, scale, do, dq, dk, dv)
     ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
     tok = _TIMER.begin("th_attn_bwd") if _TIMER is not None else None
-    L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
-                                _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
-                                _ptr(ws)))
+    if rope is not None:
+        sin, cos = _rope_tabs(q, k, rope)
+        L.check(lib.sae_th_attn_bwd_rotary(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1),
+                                           _ptr(th2), _ptr(lse), _ptr(do), _ptr(sin), _ptr(cos), _ptr(dq), _ptr(dk),
+                                           _ptr(dv), _ptr(dth1), _ptr(dth2), _ptr(ws)))
+    else:
+        L.check(lib.sae_th_attn_bwd(_stream(q), ctypes.byref(d), _ptr(q), _ptr(k), _ptr(v), _ptr(th1), _ptr(th2),
+                                    _ptr(lse), _ptr(do), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dth1), _ptr(dth2),
+                                    _ptr(ws)))
     if tok is not None:
         _TIMER.end(tok, tuple(q.shape))
     return dth1, dth2
@@ -247,11 +295,11 @@ def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale):
 
 class _TalkingHeads(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, th1, th2, scale):
+    def forward(ctx, q, k, v, th1, th2, scale, rope):
         _require_gpu(q, k, v, th1, th2)
-        o, lse, th1c, th2c = _th_fwd(q, k, v, th1, th2, scale)
+        o, lse, th1c, th2c = _th_fwd(q, k, v, th1, th2, scale, rope)
         ctx.save_for_backward(q, k, v, th1c, th2c, lse)
-        ctx.scale = scale
+        ctx.scale, ctx.rope = scale, rope
         ctx.th_dtypes = (th1.dtype, th2.dtype)
         return o
 
@@ -260,8 +308,8 @@ class _TalkingHeads(torch.autograd.Function):
         q, k, v, th1, th2, lse = ctx.saved_tensors
         do = _grad_in(do)
         dq, dk, dv = (torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in (q, k, v))
-        dth1, dth2 = _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, ctx.scale)
-        return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
+        dth1, dth2 = _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, ctx.scale, ctx.rope)
+        return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None, None
 
 
 class _TalkingHeadsPacked(torch.autograd.Function):
@@ -269,11 +317,11 @@ class _TalkingHeadsPacked(torch.autograd.Function):
     buffer through strides (no per-view gradient accumulation passes)."""
 
     @staticmethod
-    def forward(ctx, qkv, th1, th2, scale):
+    def forward(ctx, qkv, th1, th2, scale, rope):
         _require_gpu(qkv, th1, th2)
-        o, lse, th1c, th2c = _th_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, scale)
+        o, lse, th1c, th2c = _th_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, scale, rope)
         ctx.save_for_backward(qkv, th1c, th2c, lse)
-        ctx.scale = scale
+        ctx.scale, ctx.rope = scale, rope
         ctx.th_dtypes = (th1.dtype, th2.dtype)
         return o
 
@@ -283,25 +331,37 @@ class _TalkingHeadsPacked(torch.autograd.Function):
         do = _grad_in(do)
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         dth1, dth2 = _th_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, lse, do, dqkv[:, :, 0],
-                             dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale)
-        return dqkv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None
+                             dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.rope)
+        return dqkv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None, None
 
 
-def talking_heads_attention_packed(qkv, th1, th2, scale: Optional[float] = None):
-    """Talking-heads self-attention on a packed projection ``qkv`` [B, N, 3, H, D]."""
+def _th_rope_ok(q, k, v) -> bool:
+    return rope_fused_ok(q, k, v) and q.shape[2] <= L.SAE_TH_MAX_HEADS
+
+
+def talking_heads_attention_packed(qkv, th1, th2, scale: Optional[float] = None, rotary: Optional[float] = None):
+    """Talking-heads self-attention on a packed projection ``qkv`` [B, N, 3, H, D]; ``rotary`` as
+    in :func:`attention`."""
     if qkv.dim() != 5 or qkv.shape[2] != 3:
         raise ValueError(f"expected qkv [B, N, 3, H, D], got {tuple(qkv.shape)}")
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
-    return _TalkingHeadsPacked.apply(qkv, th1, th2, float(scale))
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    if rotary is not None and not _th_rope_ok(q, k, v):
+        return talking_heads_attention(q, k, v, th1, th2, scale, rotary)
+    return _TalkingHeadsPacked.apply(qkv, th1, th2, float(scale), None if rotary is None else float(rotary))
 
 
-def talking_heads_attention(q, k, v, th1, th2, scale: Optional[float] = None):
+def talking_heads_attention(q, k, v, th1, th2, scale: Optional[float] = None, rotary: Optional[float] = None):
     """Talking-heads attention (attention.py:41-58, talking_heads.py:9-14); th1/th2 are the
-    fp32 [H, H] ``talking_heads_transform`` params of TalkingHeadsBlock_0 / _1."""
+    fp32 [H, H] ``talking_heads_transform`` params of TalkingHeadsBlock_0 / _1; ``rotary`` as in
+    :func:`attention`."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    return _TalkingHeads.apply(q, k, v, th1, th2, float(scale))
+    if rotary is not None and not _th_rope_ok(q, k, v):
+        q, k = _Rotary.apply(q, float(rotary)), _Rotary.apply(k, float(rotary))
+        rotary = None
+    return _TalkingHeads.apply(q, k, v, th1, th2, float(scale), None if rotary is None else float(rotary))
 
 
 # ------------------------------------------------------------------------ relative logits
