@@ -233,9 +233,9 @@ def main():
     else:
         model = vit.create_model(args.model, 1000, torch.bfloat16, img_size=args.img_size, device=dev)
     B = args.batch
-    # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1: the
-    # eager DDP step (RCCL all-reduce overlapped with the backward through DDP's bucket hooks)
-    use_graph = world == 1 and not args.eager
+    # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1:
+    # forward + backward graph, bucketed RCCL all-reduce of the flat gradient, AdamW graph
+    use_graph = not args.eager
     step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph, input_layout=args.input_layout)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
@@ -253,8 +253,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         loss = step(images, labels)
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -310,7 +313,9 @@ def main():
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
-                   "step": "hip_graph_replay" if use_graph else "eager"},
+                   "step": ("hip_graph_replay" if world == 1 else "hip_graphs+rccl_allreduce") if use_graph
+                   else "eager"},
+        "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,
         "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,
                       "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4), "tflops": roof["tflops"],

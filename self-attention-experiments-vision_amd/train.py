@@ -2,11 +2,15 @@
 
 One process per GPU, ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm) over
 xGMI.  The reference's ``jax.pmap(train_step)`` + ``lax.pmean(grads)`` (train.py:94-96,230)
-becomes DistributedDataParallel: fp32 gradients are all-reduced in size-capped buckets in
-reverse layer order on RCCL's own stream while the backward pass is still running (the
-overlap the reference lacks, survey §3.2).  Survey D9 decisions: standard descent (the
-reference's optax chain ascends), the gradient is the global batch mean (the reference
-divides the loss by device_count *and* pmean's), no wandb call inside the step.
+becomes: every parameter's gradient is a view into ONE flat fp32 buffer; the backward of
+loss / world fills it; the buffer is all-reduced (SUM = the global-batch mean) in a few large
+buckets on RCCL; the fused AdamW steps on the views.  On the GPU the step is GPU-bound by
+construction: forward + loss + backward is one HIP graph, the optimizer a second one, and only
+the bucket all-reduces are launched eagerly between the two replays (a handful of host calls per
+step instead of the ~600 launches of an eager step, whose ~10 ms of host submission matched the
+GPU time).  Survey D9 decisions: standard descent (the reference's optax chain
+ascends), the gradient is the global batch mean (the reference divides the loss by device_count
+*and* pmean's), no wandb call inside the step.
 
 Loss: one-hot -> optax.smooth_labels(0.1) -> softmax cross-entropy, mean (train.py:83-92).
 Optimizer: Adam + decoupled weight decay 1e-4, lr 5e-4 * batch/512 (train.py:25-27,229-233;
@@ -49,30 +53,47 @@ def init_distributed():
 
 class TrainStep:
     """``step(images, labels)`` = forward (bf16 compute) + loss + backward (+ bucketed RCCL
-    all-reduce overlapped with it when world > 1) + optimizer update.  No host sync."""
+    all-reduce of the flat gradient when world > 1) + optimizer update.  No host sync.
+
+    graph=True (GPU): world == 1 -> the whole step is one HIP graph; world > 1 -> graph 1 =
+    forward + loss + backward, eager bucket all-reduces, graph 2 = AdamW."""
 
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
-                 label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
-                 graph: bool = False, input_layout: str = "NHWC"):
+                 label_smoothing: float = 0.1, bucket_cap_mb: float = 64.0, device: Optional[torch.device] = None,
+                 graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
         self.world = dist.get_world_size() if dist.is_initialized() else 1
-        # One HIP graph for the whole step (forward, loss, backward, AdamW): the eager step spends
-        # ~10 ms/step of host time submitting ~600 launches (tools/ab_step.py), as long as the GPU
-        # needs to run them.  Single-process only: with world > 1 the DDP step stays eager so the
-        # RCCL all-reduce keeps overlapping the backward through DDP's bucket hooks.
-        self.graph = bool(graph) and self.world == 1 and torch.cuda.is_available()
-        self._g = None
+        self.graph = bool(graph) and torch.cuda.is_available()
+        self._g = self._g_opt = None
         self.model = model
-        if self.world > 1:
-            self.ddp = torch.nn.parallel.DistributedDataParallel(
-                model, device_ids=[device.index] if (device is not None and device.type == "cuda") else None,
-                bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
-        else:
-            self.ddp = model
-        base_lr = lr * (global_batch / 512)
         params = [p for p in model.parameters() if p.requires_grad]
+        self._params = params
+        # flat_grads (default: world > 1) selects the multi-rank step structure: flat gradient
+        # buffer + two graphs around the all-reduce (settable at world 1 to test that structure)
+        self.flat = self.world > 1 if flat_grads is None else bool(flat_grads)
+        if self.flat:
+            # one flat fp32 gradient buffer, every .grad a view into it (autograd accumulates into
+            # the views in place), cut into buckets of ~bucket_cap_mb along parameter boundaries
+            # in reverse registration order (the order the backward finishes them)
+            n = sum(p.numel() for p in params)
+            dev = params[0].device
+            self._flat = torch.zeros(n, dtype=torch.float32, device=dev)
+            off = 0
+            for p in params:
+                p.grad = self._flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            cap = max(1, int(bucket_cap_mb * 2 ** 20 / 4))
+            self._buckets, hi, lo = [], n, n
+            for p in reversed(params):
+                lo -= p.numel()
+                if hi - lo >= cap:   # close a bucket once it holds >= cap elements
+                    self._buckets.append((lo, hi))
+                    hi = lo
+            if hi > 0:
+                self._buckets.append((0, hi))
+        base_lr = lr * (global_batch / 512)
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         if self.graph:
             kw["capturable"] = True   # step counters on the device: replayable
@@ -82,21 +103,51 @@ class TrainStep:
             self.opt = torch.optim.AdamW(params, foreach=True, **kw)
         self.smoothing = label_smoothing
 
-    def _eager(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        self.opt.zero_grad(set_to_none=True)
-        if self.input_layout == "NHWC":
-            logits = self.ddp(images, is_training=True)
+    # ---- pieces of one step
+    def _zero_grad(self):
+        if self.flat:
+            self._flat.zero_()
         else:
-            logits = self.ddp(images, is_training=True, layout=self.input_layout)
+            self.opt.zero_grad(set_to_none=True)
+
+    def _fwd_bwd(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        self._zero_grad()
+        if self.input_layout == "NHWC":
+            logits = self.model(images, is_training=True)
+        else:
+            logits = self.model(images, is_training=True, layout=self.input_layout)
         loss = smoothed_cross_entropy(logits, labels, self.smoothing)
-        loss.backward()
-        self.opt.step()
+        # world > 1: the SUM all-reduce of the per-rank gradients of loss / world is the
+        # gradient of the global-batch mean (survey D9)
+        (loss / self.world if self.world > 1 else loss).backward()
         return loss.detach()
+
+    def _allreduce(self):
+        if self.world == 1:
+            return
+        if self._flat.is_cuda and dist.get_backend() == "gloo":
+            # rehearsal of the multi-rank step on fewer GPUs (SAE_DIST_BACKEND=gloo): one explicit
+            # host round trip (gloo's own CUDA path stalled for seconds behind the graph replays)
+            host = self._flat.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            self._flat.copy_(host)
+            return
+        # RCCL: every bucket in flight at once on the process group's stream; the optimizer's
+        # graph replay waits for them on the compute stream (no host synchronisation)
+        works = [dist.all_reduce(self._flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True) for lo, hi in self._buckets]
+        for w in works:
+            w.wait()
+
+    def _eager(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        loss = self._fwd_bwd(images, labels)
+        self._allreduce()
+        self.opt.step()
+        return loss
 
     def _capture(self, images: torch.Tensor, labels: torch.Tensor):
         self._images = images.clone()
         self._labels = labels.clone()
-        params = [p for p in self.model.parameters() if p.requires_grad]
+        params = self._params
         snap = [p.detach().clone() for p in params]
         had_state = {id(p) for p in params if p in self.opt.state and self.opt.state[p]}
         snap_state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
@@ -125,18 +176,27 @@ class TrainStep:
                         v.copy_(old[k])
                     else:   # state created by the warm-up: a fresh optimizer's zeros
                         v.zero_()
-        g = torch.cuda.CUDAGraph()
-        self.opt.zero_grad(set_to_none=True)
+        if not self.flat:
+            self.opt.zero_grad(set_to_none=True)
         try:
-            with torch.cuda.graph(g):
-                self._loss = self._eager(self._images, self._labels)
+            if not self.flat:     # the whole step in one graph
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._loss = self._eager(self._images, self._labels)
+                self._g = g
+            else:                 # the collectives stay outside: two graphs around them
+                g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._loss = self._fwd_bwd(self._images, self._labels)
+                with torch.cuda.graph(go):
+                    self.opt.step()
+                self._g, self._g_opt = g, go
         except RuntimeError as e:   # an op that cannot be captured: stay eager, say so once
             import sys
             print(f"[train] HIP-graph capture failed ({e}); running the eager step", file=sys.stderr)
             self.graph = False
+            self._g = self._g_opt = None
             torch.cuda.synchronize()
-            return
-        self._g = g
 
     def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         if not self.graph:
@@ -150,4 +210,7 @@ class TrainStep:
         if labels.data_ptr() != self._labels.data_ptr():
             self._labels.copy_(labels)
         self._g.replay()
+        if self._g_opt is not None:
+            self._allreduce()
+            self._g_opt.replay()
         return self._loss

@@ -1,9 +1,10 @@
 """Multi-process data-parallel path on CPU (gloo, world size 2).
 
 The training step (sae_vision_amd.train.TrainStep, the rebuild of the reference's
-pmap(train_step) + lax.pmean(grads), train.py:94-96,230) must give every rank the same
-parameters as a single process stepping on the concatenated global batch (global-mean gradient,
-survey D9).  The attention kernels themselves are replicas (GPU only); this checks the
+pmap(train_step) + lax.pmean(grads), train.py:94-96,230: flat gradient buffer, bucketed SUM
+all-reduce of the gradients of loss / world) must give every rank the same parameters as a
+single process stepping on the concatenated global batch (global-mean gradient, survey D9).
+The GPU step runs the same code between its two HIP graphs.  The attention kernels themselves are replicas (GPU only); this checks the
 collective / bucketing / optimizer path with a small CPU model.
 """
 import os
@@ -40,7 +41,13 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x, y = _data()
     per = x.shape[0] // world
-    step = train.TrainStep(TinyNet(), global_batch=x.shape[0], bucket_cap_mb=0.001)
+    step = train.TrainStep(TinyNet(), global_batch=x.shape[0], bucket_cap_mb=0.0001)
+    # the flat gradient buffer: every .grad a view into it, buckets tile it from the end (the
+    # order the backward completes the parameters), each at least the cap unless it is the last
+    n = sum(p.numel() for p in step.model.parameters())
+    b = step._buckets
+    assert b[0][1] == n and b[-1][0] == 0 and all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+    assert len(b) > 1 and all(p.grad.data_ptr() >= step._flat.data_ptr() for p in step.model.parameters())
     for _ in range(3):
         step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
     flat = torch.cat([p.detach().flatten() for p in step.model.parameters()])
