@@ -327,7 +327,7 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
 // bf16 with the head mixes on the MFMA (th2.h); NWMAX = 8 or 16 waves per workgroup
 template <int DP, int NWMAX, bool ROT> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32;
-  const size_t lds = th2_lds_bytes<DP>(a.H);
+  const size_t lds = th2_lds_bytes<DP, NWMAX <= 8>(a.H);
   if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT>, lds)) return rc;
   hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
   return check_launch("th2_fwd");
@@ -336,7 +336,7 @@ template <int DP, int NWMAX, bool ROT> int th2_fwd_run(hipStream_t st, const ThA
 template <int DP, int NWMAX, bool ROT> int th2_bwd_run(hipStream_t st, ThArgs a) {
   const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32;
   a.nblk = nqb * a.B;
-  const size_t lds = th2_lds_bytes<DP>(a.H), lds_kv = th2_kv_lds_bytes<DP>(a.H, NWMAX <= 8);
+  const size_t lds = th2_lds_bytes<DP, NWMAX <= 8>(a.H), lds_kv = th2_kv_lds_bytes<DP, NWMAX <= 8>(a.H, NWMAX <= 8);
   if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT>, lds)) return rc;
   if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT>, lds_kv)) return rc;
   hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);

@@ -31,8 +31,19 @@
 namespace sae {
 
 constexpr int kTh2MaxH = 16;
-constexpr int kTh2Row = 2112;                    // bytes per head row: 1024 bf16 + 64 B pad
-constexpr int kTh2Img = kTh2MaxH * kTh2Row;      // one exchange image (33 KiB)
+// An image row (one head) holds 1024 positions = 32 blocks of 32 bf16; each block is padded to
+// 80 bytes (a multiple of 16 for the 16-byte reads), so that the lanes of a transposed tile write
+// (lane = block, four consecutive positions each) spread over the banks instead of sharing 8;
+// head rows are 64 bytes (16 banks) past a multiple of 256, so that the mixes' transposed reads
+// (4 head rows x 64 contiguous bytes) and the dT reads (one 16-byte piece per head row) do not
+// pile onto the same banks (with rows a multiple of 256 bytes apart they conflicted 4- to 16-way)
+constexpr int kTh2Blk = 80;                      // bytes per 32-position block
+constexpr int kTh2Row = 32 * kTh2Blk + 64;       // bytes per head row (2624 = 10 x 256 + 64)
+// KST ("K-stacked", H <= 8): a mix is ONE MFMA whose K = 16 holds the 8 heads twice, the high
+// bf16 part of T against the first copy and the low part against the second, and the images
+// need only 8 rows; otherwise (H <= 16) two MFMAs (high, low) over 16 image rows.
+template <bool KST> constexpr int th2_rows() { return KST ? 8 : kTh2MaxH; }
+template <bool KST> constexpr int th2_img() { return th2_rows<KST>() * kTh2Row; }   // one exchange image
 constexpr int kTh2MixTbl = 4 * 64 * 32;          // th2_bwd_kv: four mix operands (hi, lo) per lane
 
 typedef __attribute__((ext_vector_type(8))) short th_s16x8;
@@ -47,75 +58,102 @@ __device__ __forceinline__ bf16x8 th2_tr2(const char* p1, const char* p2) {
 // A operand of a head mix, high and low bf16 parts: A[row][k] = TR ? T[row][k] : T[k][row]
 // (T fp32 [H][H], [h_in][h_out]).  K order: standard (k = 8 (lane >> 5) + j: the B operand comes
 // from an image) or PERM (the B operand is a 32 x 32 accumulator: element j of lane half g is
-// row 8 (j >> 2) + 4 g + (j & 3)).  Rows / k >= H are zero.
+// row 8 (j >> 2) + 4 g + (j & 3)).  Rows / k >= H are zero.  KST: one operand in `hi` whose k < 8
+// carry the high parts of heads k and k >= 8 the low parts of heads k - 8.
 struct Th2Mix {
   bf16x8 hi, lo;
 };
-template <bool TR, bool PERM>
+template <bool TR, bool PERM, bool KST>
 __device__ __forceinline__ Th2Mix th2_mix(const float* T, int H, int lane) {
   Th2Mix m;
   const int row = lane & 31, g = lane >> 5;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = PERM ? 8 * (j >> 2) + 4 * g + (j & 3) : 8 * g + j;
-    const float t = (row < H && k < H) ? (TR ? T[row * H + k] : T[k * H + row]) : 0.f;
+    const int hd = KST ? (k & 7) : k;
+    const float t = (row < H && hd < H) ? (TR ? T[row * H + hd] : T[hd * H + row]) : 0.f;
     const __bf16 hi = (__bf16)t;
-    m.hi[j] = hi;
-    m.lo[j] = (__bf16)(t - (float)hi);
+    const __bf16 lo = (__bf16)(t - (float)hi);
+    if constexpr (KST) {
+      m.hi[j] = k < 8 ? hi : lo;
+      m.lo[j] = (__bf16)0.f;
+    } else {
+      m.hi[j] = hi;
+      m.lo[j] = lo;
+    }
   }
   return m;
 }
 
 // mixed tile of position block `blk` (32 positions) from an image: C[row][pos], pos on the lane
+template <bool KST>
 __device__ __forceinline__ f32x16 th2_mix_img(const char* img, int blk, const Th2Mix& m, int lane) {
   const int li = lane & 15;
-  const int r1 = 8 * (lane >> 5) + (li >> 2);
-  const int col = blk * 32 + 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-  const bf16x8 b = th2_tr2(img + r1 * kTh2Row + col * 2, img + (r1 + 4) * kTh2Row + col * 2);
-  f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
+  const int r1 = (KST ? 0 : 8 * (lane >> 5)) + (li >> 2);   // KST: both lane halves read rows 0..7
+  const int col = blk * kTh2Blk + (16 * ((lane >> 4) & 1) + 4 * (li & 3)) * 2;
+  const bf16x8 b = th2_tr2(img + r1 * kTh2Row + col, img + (r1 + 4) * kTh2Row + col);
+  const f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
+  if constexpr (KST) return c;
   return MF<__bf16>::mma(m.lo, b, c);
 }
 
-// mixed tile from an accumulator (rows = heads < 16, lanes = positions)
+// mixed tile from an accumulator (rows = heads < 16, lanes = positions); KST: registers 4..7
+// (rows 8..15) take a copy of 0..3 (rows 0..7), the second K half of the stacked operand
+template <bool KST>
 __device__ __forceinline__ f32x16 th2_mix_acc(const f32x16& x, const Th2Mix& m) {
-  const bf16x8 b = acc_frag<__bf16>(x, 0);
-  f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
-  return MF<__bf16>::mma(m.lo, b, c);
-}
-
-// bf16 tile (accumulator layout: row row_of(r, h) on register r, column on the lane) into image
-// row `head`; every position pos = row * 32 + column.
-__device__ __forceinline__ void th2_put(char* img, int head, const f32x16& v, float sc, int lane) {
-  __bf16* p = reinterpret_cast<__bf16*>(img + head * kTh2Row) + (lane & 31);
-  const int h = lane >> 5;
+  if constexpr (KST) {
+    f32x16 y = x;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) p[row_of(r, h) * 32] = (__bf16)(v[r] * sc);
-}
-
-// rows i < H of a mixed block (accumulator rows = heads) into the images at block `blk`
-__device__ __forceinline__ void th2_put_block(char* img, int blk, const f32x16& v, int H, int lane) {
-  __bf16* p = reinterpret_cast<__bf16*>(img) + blk * 32 + (lane & 31);
-  const int h = lane >> 5;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = row_of(r, h);
-    if (i < H) p[i * (kTh2Row / 2)] = (__bf16)v[r];
+    for (int r = 0; r < 4; ++r) y[4 + r] = x[r];
+    return MF<__bf16>::mma(m.hi, acc_frag<__bf16>(y, 0), zero16());
+  } else {
+    const bf16x8 b = acc_frag<__bf16>(x, 0);
+    f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
+    return MF<__bf16>::mma(m.lo, b, c);
   }
 }
 
-// zero image rows [H, 16) once (read as the padded k of the mixes; must be finite)
+// bf16 score tile in the transposed accumulator layout (query row_of(r, h) on register r, key on
+// the lane) into image row `head` at position key * 32 + query: registers 4g .. 4g + 3 are four
+// consecutive positions, one 8-byte write
+__device__ __forceinline__ void th2_put(char* img, int head, const f32x16& v, float sc, int lane) {
+  char* p = img + head * kTh2Row + (lane & 31) * kTh2Blk + 8 * (lane >> 5);
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<bf16x4*>(p + 16 * g) = bf16x4{(__bf16)(v[4 * g] * sc), (__bf16)(v[4 * g + 1] * sc),
+                                                   (__bf16)(v[4 * g + 2] * sc), (__bf16)(v[4 * g + 3] * sc)};
+}
+
+// rows i < H of a mixed block (accumulator rows = heads; registers r < NR) into the images at
+// block `blk`
+template <int NR>
+__device__ __forceinline__ void th2_put_block(char* img, int blk, const f32x16& v, int H, int lane) {
+  char* p = img + blk * kTh2Blk + (lane & 31) * 2;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int i = row_of(r, h);
+    if (i < H) *reinterpret_cast<__bf16*>(p + i * kTh2Row) = (__bf16)v[r];
+  }
+}
+
+// zero image rows [H, rows) once (read as the padded k of the mixes; must be finite)
+template <bool KST>
 __device__ __forceinline__ void th2_zero_pad(char* img, int H, int tid, int nthreads) {
   uint4* p = reinterpret_cast<uint4*>(img + H * kTh2Row);
-  const int n = (kTh2MaxH - H) * kTh2Row / 16;
+  const int n = (th2_rows<KST>() - H) * kTh2Row / 16;
   for (int i = tid; i < n; i += nthreads) p[i] = uint4{0, 0, 0, 0};
 }
 
 // 16 x 16 dT partial for position block blk: acc[h = 4 (lane >> 4) + j][i = lane & 15] +=
 // sum over the block's 32 positions of A-image[h] * B-image[i]
+template <bool KST>
 __device__ __forceinline__ f32x4 th2_dt(const char* ia, const char* ib, int blk, f32x4 acc, int lane) {
-  const int row = lane & 15, k0 = blk * 32 + 8 * (lane >> 4);
-  const bf16x8 a = *reinterpret_cast<const bf16x8*>(ia + row * kTh2Row + k0 * 2);
-  const bf16x8 b = *reinterpret_cast<const bf16x8*>(ib + row * kTh2Row + k0 * 2);
+  // KST: 8-row images; lanes 8..15 re-read rows 0..7 (their dT rows / columns are discarded)
+  const int row = lane & (KST ? 7 : 15), o = blk * kTh2Blk + 16 * (lane >> 4);
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(ia + row * kTh2Row + o);
+  const bf16x8 b = *reinterpret_cast<const bf16x8*>(ib + row * kTh2Row + o);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
@@ -126,15 +164,15 @@ __device__ __forceinline__ f32x4 th2_dt(const char* ia, const char* ib, int blk,
 __device__ __forceinline__ bf16x8 th2_colB(const char* img, int head, int s, int lane) {
   const int li = lane & 15;
   const int r1 = 16 * s + 4 * (lane >> 5) + (li >> 2);
-  const int col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-  const char* base = img + head * kTh2Row;
-  return th2_tr2(base + (r1 * 32 + col) * 2, base + ((r1 + 8) * 32 + col) * 2);
+  const int col = (16 * ((lane >> 4) & 1) + 4 * (li & 3)) * 2;
+  const char* base = img + head * kTh2Row + col;
+  return th2_tr2(base + r1 * kTh2Blk, base + (r1 + 8) * kTh2Blk);
 }
 
 // th2_rowB: image row `head` read as a [column = lane][row] matrix (position = column * 32 + row:
 // the key-block kernel, B[k = query][column = key]): two 8-byte reads of query runs
 __device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int lane) {
-  const char* base = img + head * kTh2Row + ((lane & 31) * 32 + 16 * s + 4 * (lane >> 5)) * 2;
+  const char* base = img + head * kTh2Row + (lane & 31) * kTh2Blk + (16 * s + 4 * (lane >> 5)) * 2;
   const s16x4 x1 = *reinterpret_cast<const s16x4*>(base);
   const s16x4 x2 = *reinterpret_cast<const s16x4*>(base + 16);
   const th_s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
@@ -159,17 +197,23 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
 }
 
 // ================================================================================= forward
+// (Measured and dropped: double-buffered images with the next tile's scores issued before this
+// tile's mixes and one barrier per tile -- 238 vs 221 us at cait_s24: in-order issue stalls on
+// the score tile's MFMA results before the mixes can start, so nothing overlapped.)
 template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
+  constexpr bool KST = NWMAX <= 8;           // H <= 8: stacked mixes, heads in registers 0..3
+  constexpr int NR = KST ? 4 : 8;            // registers r < NR hold the mixed heads row_of(r, h)
+  constexpr int IMG = th2_img<KST>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* XS = smem;                          // scores S_h (bf16), then statistics scratch
-  char* XP = smem + kTh2Img;                // mixed probabilities P2_j (bf16)
-  char* ldsV = smem + 2 * kTh2Img + w * I::bytes(32);
+  char* const XS = smem;                    // scores S_h (bf16), then statistics scratch
+  char* const XP = smem + IMG;              // mixed probabilities P2_j (bf16)
+  char* ldsV = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
   const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
@@ -178,24 +222,25 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
 
-  th2_zero_pad(XS, H, tid, 64 * H);
-  th2_zero_pad(XP, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * H);
+  th2_zero_pad<KST>(XP, H, tid, 64 * H);
   constexpr bool rot = ROT;   // rotary: q / k rotated as they are loaded
+  const bool full = a.D > 16 * (NS - 1);   // the last 16-wide k-step holds head-dim columns
   bf16x8 qf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
     if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
   }
-  const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);   // S1 = T1^T S
-  const Th2Mix m2 = th2_mix<false, true>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
+  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);   // S1 = T1^T S
+  const Th2Mix m2 = th2_mix<false, true, KST>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
   const int nkt = (a.Nk + 31) / 32;
 
   // ---- pass 0: row statistics (log2 domain) of the mixed logits, per (head i, query) in this
   //      wave's key blocks: register r <-> head row_of(r, h), lane <-> query
-  float m[8], l[8];
+  float m[NR], l[NR];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < NR; ++r) {
     m[r] = -kInf;
     l[r] = 0.f;
   }
@@ -213,36 +258,56 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
     load_k(kt + 1 < nkt ? kt + 1 : 0);
     f32x16 s = zero16();
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) s = MF<__bf16>::mma(kc[s_], qf[s_], s);
+    for (int s_ = 0; s_ < NS; ++s_)
+      if (s_ < NS - 1 || full) s = MF<__bf16>::mma(qf[s_], kc[s_], s);   // S^T: query rows, key lanes
     th2_put(XS, w, s, a.scale, lane);
+  };
+  auto stats = [&](int kt) {   // this wave's blocks of tile kt, groups of four: one max update each
+    const char* xs = XS;
+    for (int b0 = w; b0 < 32; b0 += 4 * H) {
+      f32x16 c[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // independent chains: issued together, blocks past the end clamped
+        const int blk = b0 + u * H;
+        ok[u] = blk < 32 && kt * 32 + blk < a.Nk;
+        c[u] = th2_mix_img<KST>(xs, blk & 31, m1, lane);
+      }
+      if (!ok[0]) break;   // (the later blocks of the group lie further out)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        float mx = -kInf;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ok[u]) mx = fmaxf(mx, c[u][r]);
+        const float mn = fmaxf(m[r], mx * kLog2e);
+        float sum = l[r] * ex2(m[r] - mn);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ok[u]) sum += ex2(__builtin_fmaf(c[u][r], kLog2e, -mn));
+        l[r] = sum;
+        m[r] = mn;
+      }
+    }
   };
   load_k(0);
   for (int kt = 0; kt < nkt; ++kt) {
     scores(kt);
     __syncthreads();
-    for (int blk = w; blk < 32 && kt * 32 + blk < a.Nk; blk += H) {
-      const f32x16 c = th2_mix_img(XS, blk, m1, lane);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float x = c[r] * kLog2e;
-        const float mn = fmaxf(m[r], x);
-        l[r] = l[r] * ex2(m[r] - mn) + ex2(x - mn);
-        m[r] = mn;
-      }
-    }
+    stats(kt);
     __syncthreads();
   }
-  // combine the per-wave statistics: scratch [w][r][lane] (m, l) in the two images
+  // combine the per-wave statistics: scratch [w][r][lane] (m, l) in the images
   {
     float2* st = reinterpret_cast<float2*>(smem);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) st[(w * 8 + r) * 64 + lane] = make_float2(m[r], l[r]);
+    for (int r = 0; r < NR; ++r) st[(w * NR + r) * 64 + lane] = make_float2(m[r], l[r]);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < NR; ++r) {
       float mm = -kInf, ll = 0.f;
       for (int ww = 0; ww < H; ++ww) {
-        const float2 v = st[(ww * 8 + r) * 64 + lane];
+        const float2 v = st[(ww * NR + r) * 64 + lane];
         const float mn = fmaxf(mm, v.x);
         ll = (mm == -kInf ? 0.f : ll * ex2(mm - mn)) + (v.x == -kInf ? 0.f : v.y * ex2(v.x - mn));
         mm = mn;
@@ -253,42 +318,57 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       if (w == 0 && i < H && q < a.Nq) a.lse[((size_t)b * H + i) * a.Nq + q] = (mm + lg2(ll)) * kLn2;
     }
     __syncthreads();
-    th2_zero_pad(XS, H, tid, 64 * H);   // the scratch overwrote the pad rows
-    th2_zero_pad(XP, H, tid, 64 * H);
+    th2_zero_pad<KST>(XS, H, tid, 64 * H);   // the scratch overwrote the pad rows
+    th2_zero_pad<KST>(XP, H, tid, 64 * H);
   }
 
   // ---- pass 1: P_i = 2^(S1 - m) / l, P2 = T2^T P into XP, O_w += P2_w V_w
   f32x16 acco[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acco[t] = zero16();
-  WStage<__bf16, DP, true> vst;   // V tile kt + 1 in flight while tile kt computes
-  vst.load(V, 0, a.Nk, a.vs[1], a.D, lane);
-  vst.write(ldsV, lane);
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vst.load(V, (kt + 1) * 32, a.Nk, a.vs[1], a.D, lane);
-    scores(kt);
-    __syncthreads();
-    for (int blk = w; blk < 32; blk += H) {
-      f32x16 p2;
-      if (kt * 32 + blk < a.Nk) {
-        f32x16 c = th2_mix_img(XS, blk, m1, lane);
+  auto probs = [&](int kt) {   // this wave's blocks of tile kt: P2 = T2^T P into XP
+    const char* xs = XS;
+    char* xp = XP;
+    constexpr int G = KST ? 4 : 2;   // blocks per group: independent chains issued together
+    for (int b0 = w; b0 < 32; b0 += G * H) {
+      f32x16 c[G];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) c[r] = ex2(c[r] * kLog2e - m[r]) * l[r];
+      for (int u = 0; u < G; ++u) c[u] = th2_mix_img<KST>(xs, (b0 + u * H) & 31, m1, lane);
 #pragma unroll
-        for (int r = 8; r < 16; ++r) c[r] = 0.f;
-        p2 = th2_mix_acc(c, m2);
-      } else {
-        p2 = zero16();   // keys past the end: P2 = 0
+      for (int u = 0; u < G; ++u) {
+        const int blk = b0 + u * H;
+        const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: P = 0
+#pragma unroll
+        for (int r = 0; r < NR; ++r) c[u][r] = ok ? ex2(__builtin_fmaf(c[u][r], kLog2e, -m[r])) * l[r] : 0.f;
+        if constexpr (!KST) {
+#pragma unroll
+          for (int r = 8; r < 16; ++r) c[u][r] = 0.f;
+        }
+        c[u] = th2_mix_acc<KST>(c[u], m2);
       }
-      th2_put_block(XP, blk, p2, H, lane);
+#pragma unroll
+      for (int u = 0; u < G; ++u)
+        if (b0 + u * H < 32) th2_put_block<NR>(xp, b0 + u * H, c[u], H, lane);
     }
-    __syncthreads();
+  };
+  auto pv = [&]() {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pf = th2_colB(XP, w, s2, lane);
 #pragma unroll
       for (int t = 0; t < NT; ++t) acco[t] = MF<__bf16>::mma(I::colfrag(ldsV, 0, s2, 32 * t, lane), pf, acco[t]);
     }
+  };
+  WStage<__bf16, DP, true> vst;   // V tile kt + 1 in flight while tile kt computes (wave-private image)
+  vst.load(V, 0, a.Nk, a.vs[1], a.D, lane);
+  vst.write(ldsV, lane);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) vst.load(V, (kt + 1) * 32, a.Nk, a.vs[1], a.D, lane);
+    scores(kt);
+    __syncthreads();
+    probs(kt);
+    __syncthreads();
+    pv();
     if (kt + 1 < nkt) vst.write(ldsV, lane);   // wave-private: after this wave's own reads
     __syncthreads();
   }
@@ -310,13 +390,16 @@ template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
+  constexpr bool KST = NWMAX <= 8;
+  constexpr int NR = KST ? 4 : 8;
+  constexpr int IMG = th2_img<KST>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* XS = smem;
-  char* XG = smem + kTh2Img;
-  char* ldsK = smem + 2 * kTh2Img + w * I::bytes(32);
+  char* XG = smem + IMG;
+  char* ldsK = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
   const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
@@ -326,9 +409,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
 
-  th2_zero_pad(XS, H, tid, 64 * H);
-  th2_zero_pad(XG, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * H);
+  th2_zero_pad<KST>(XG, H, tid, 64 * H);
   constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dq rotated back
+  const bool full = a.D > 16 * (NS - 1);
   bf16x8 qf[NS], gf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -336,13 +420,13 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
     gf[s] = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s, h);
   }
-  const Th2Mix m1 = th2_mix<false, false>(a.th1, H, lane);    // S1 = T1^T S        (image)
-  const Th2Mix m2t = th2_mix<true, false>(a.th2, H, lane);    // dP = T2 dP2        (image)
-  const Th2Mix m1t = th2_mix<true, true>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
+  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);    // S1 = T1^T S        (image)
+  const Th2Mix m2t = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
+  const Th2Mix m1t = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
   // lse (log2 domain) of the mixed rows of this lane's query, register r <-> head row_of(r, h)
-  float lse2[8];
+  float lse2[NR];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < NR; ++r) {
     const int i = row_of(r, h);
     lse2[r] = (i < H && q < a.Nq) ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
   }
@@ -366,8 +450,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     f32x16 s = zero16(), g = zero16();
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
-      s = MF<__bf16>::mma(kc[s_], qf[s_], s);
-      g = MF<__bf16>::mma(vc[s_], gf[s_], g);
+      if (s_ < NS - 1 || full) {   // S^T, dP2^T: query rows, key lanes
+        s = MF<__bf16>::mma(qf[s_], kc[s_], s);
+        g = MF<__bf16>::mma(gf[s_], vc[s_], g);
+      }
     }
     th2_put(XS, w, s, a.scale, lane);
     th2_put(XG, w, g, 1.f, lane);
@@ -375,23 +461,35 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   load_kv(0);
 
   // ---- pass A
-  float dl[8];
+  float dl[NR];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) dl[r] = 0.f;
+  for (int r = 0; r < NR; ++r) dl[r] = 0.f;
   f32x4 dt2 = {0.f, 0.f, 0.f, 0.f};
   for (int kt = 0; kt < nkt; ++kt) {
     tiles(kt);
     __syncthreads();
-    for (int blk = w; blk < 32 && kt * 32 + blk < a.Nk; blk += H) {
-      f32x16 p = th2_mix_img(XS, blk, m1, lane);
-      const f32x16 dp = th2_mix_img(XG, blk, m2t, lane);
+    constexpr int G = 2;   // blocks per group: independent chains issued together
+    for (int b0 = w; b0 < 32 && kt * 32 + b0 < a.Nk; b0 += G * H) {
+      f32x16 p[G], dp[G];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        p[r] = ex2(p[r] * kLog2e - lse2[r]);
-        dl[r] += p[r] * dp[r];
+      for (int u = 0; u < G; ++u) {
+        p[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, m1, lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, m2t, lane);
       }
-      th2_put_block(XS, blk, p, H, lane);   // P over S at this block (only this wave touches it)
-      dt2 = th2_dt(XS, XG, blk, dt2, lane);  // dT2[h][i] += sum P_h dP2_i
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int blk = b0 + u * H;
+        const bool ok = blk < 32 && kt * 32 + blk < a.Nk;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          p[u][r] = ex2(__builtin_fmaf(p[u][r], kLog2e, -lse2[r]));
+          dl[r] += ok ? p[u][r] * dp[u][r] : 0.f;
+        }
+        if (ok) {
+          th2_put_block<NR>(XS, blk, p[u], H, lane);   // P over S at this block (only this wave touches it)
+          dt2 = th2_dt<KST>(XS, XG, blk, dt2, lane);   // dT2[h][i] += sum P_h dP2_i
+        }
+      }
     }
     __syncthreads();
   }
@@ -399,12 +497,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   {
     float* st = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) st[(w * 8 + r) * 64 + lane] = dl[r];
+    for (int r = 0; r < NR; ++r) st[(w * NR + r) * 64 + lane] = dl[r];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < NR; ++r) {
       float s = 0.f;
-      for (int ww = 0; ww < H; ++ww) s += st[(ww * 8 + r) * 64 + lane];
+      for (int ww = 0; ww < H; ++ww) s += st[(ww * NR + r) * 64 + lane];
       dl[r] = s;
       const int i = row_of(r, h);
       if (w == 0 && i < H && q < a.Nq) a.delta[((size_t)b * H + i) * a.Nq + q] = s;
@@ -413,8 +511,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   }
   float* pb = a.part + (size_t)blockIdx.x * 2 * H * H;
   th2_dt_store(reinterpret_cast<float*>(smem), dt2, pb + H * H, H, w, lane, tid, false);
-  th2_zero_pad(XS, H, tid, 64 * H);
-  th2_zero_pad(XG, H, tid, 64 * H);   // (the last tile of pass A prefetched key tile 0)
+  th2_zero_pad<KST>(XS, H, tid, 64 * H);
+  th2_zero_pad<KST>(XG, H, tid, 64 * H);   // (the last tile of pass A prefetched key tile 0)
 
   // ---- pass B
   f32x16 adq[NT];
@@ -428,19 +526,30 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     if (rot) kst.rope(a.rope, kt * 32, lane);
     kst.write(ldsK, lane);
     __syncthreads();
-    for (int blk = w; blk < 32; blk += H) {
-      if (kt * 32 + blk < a.Nk) {
-        f32x16 ds1 = th2_mix_img(XS, blk, m1, lane);
-        const f32x16 dp = th2_mix_img(XG, blk, m2t, lane);
+    constexpr int G = 2;
+    for (int b0 = w; b0 < 32; b0 += G * H) {
+      f32x16 ds1[G], dp[G];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) ds1[r] = ex2(ds1[r] * kLog2e - lse2[r]) * (dp[r] - dl[r]);
+      for (int u = 0; u < G; ++u) {
+        ds1[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, m1, lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, m2t, lane);
+      }
 #pragma unroll
-        for (int r = 8; r < 16; ++r) ds1[r] = 0.f;
-        th2_put_block(XG, blk, ds1, H, lane);   // dS1 over dP2 at this block
-        dt1 = th2_dt(XS, XG, blk, dt1, lane);    // dT1[h][i] += sum S_h dS1_i
-        th2_put_block(XS, blk, th2_mix_acc(ds1, m1t), H, lane);   // dS_h over S_h
-      } else {
-        th2_put_block(XS, blk, zero16(), H, lane);
+      for (int u = 0; u < G; ++u) {
+        const int blk = b0 + u * H;
+        const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: dS = 0
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          ds1[u][r] = ok ? ex2(__builtin_fmaf(ds1[u][r], kLog2e, -lse2[r])) * (dp[u][r] - dl[r]) : 0.f;
+        if constexpr (!KST) {
+#pragma unroll
+          for (int r = 8; r < 16; ++r) ds1[u][r] = 0.f;
+        }
+        if (blk < 32) {
+          th2_put_block<NR>(XG, blk, ds1[u], H, lane);   // dS1 over dP2 at this block
+          if (ok) dt1 = th2_dt<KST>(XS, XG, blk, dt1, lane);   // dT1[h][i] += sum S_h dS1_i
+          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(ds1[u], m1t), H, lane);   // dS_h over S_h
+        }
       }
     }
     __syncthreads();
@@ -480,13 +589,16 @@ template <int DP, int NWMAX, bool ROT = false>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
+  constexpr bool KST = NWMAX <= 8;
+  constexpr int NR = KST ? 4 : 8;
+  constexpr int IMG = th2_img<KST>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* XS = smem;
-  char* XG = smem + kTh2Img;
-  char* MX = smem + 2 * kTh2Img;   // the four mix operands, per lane (registers are short here)
+  char* XG = smem + IMG;
+  char* MX = smem + 2 * IMG;   // the four mix operands, per lane (registers are short here)
   char* buf = MX + kTh2MixTbl + w * I::bytes(32);
 
   const int nkb = (a.Nk + 31) / 32;
@@ -497,9 +609,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
 
-  th2_zero_pad(XS, H, tid, 64 * H);
-  th2_zero_pad(XG, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * H);
+  th2_zero_pad<KST>(XG, H, tid, 64 * H);
   constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dk rotated back
+  const bool full = a.D > 16 * (NS - 1);
   bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -509,10 +622,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   }
   if (w == 0) {
     Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
-    mx[0 * 64 + lane] = th2_mix<false, false>(a.th1, H, lane);   // T1^T, image operand
-    mx[1 * 64 + lane] = th2_mix<false, true>(a.th2, H, lane);    // T2^T, accumulator operand
-    mx[2 * 64 + lane] = th2_mix<true, false>(a.th2, H, lane);    // T2, image operand
-    mx[3 * 64 + lane] = th2_mix<true, true>(a.th1, H, lane);     // T1, accumulator operand
+    mx[0 * 64 + lane] = th2_mix<false, false, KST>(a.th1, H, lane);   // T1^T, image operand
+    mx[1 * 64 + lane] = th2_mix<false, true, KST>(a.th2, H, lane);    // T2^T, accumulator operand
+    mx[2 * 64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);    // T2, image operand
+    mx[3 * 64 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);     // T1, accumulator operand
   }
   const Th2Mix* mx = reinterpret_cast<const Th2Mix*>(MX) + lane;
   f32x16 adk[NT], adv[NT];
@@ -546,9 +659,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
       gst.load(G, qt * 32, a.Nq, a.dos[1], a.D, lane);
       qst.load(Q, qt * 32, a.Nq, a.qs[1], a.D, lane);
     }
-    float lse2[8], dl[8];
+    float lse2[NR], dl[NR];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int i = row_of(r, h);
       const bool ok = i < H && q < a.Nq;
       lse2[r] = ok ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
@@ -567,37 +680,46 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
           if (rot) qa = rope8<1>(qa, a.rope, q, 16 * s_ + 8 * h);
           ga = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s_, h);
         }
-        s = MF<__bf16>::mma(kf[s_], qa, s);
-        g = MF<__bf16>::mma(vf[s_], ga, g);
+        if (s_ < NS - 1 || full) {   // query rows, key lanes (th2_put)
+          s = MF<__bf16>::mma(qa, kf[s_], s);
+          g = MF<__bf16>::mma(ga, vf[s_], g);
+        }
       }
       th2_put(XS, w, s, a.scale, lane);
       th2_put(XG, w, g, 1.f, lane);
     }
     if constexpr (!TWO) gst.write(buf, lane);
     __syncthreads();
-    for (int blk = w; blk < 32; blk += H) {   // blk = key of this block
-      f32x16 p2, ds;
-      if (kb * 32 + blk < a.Nk) {
-        f32x16 p = th2_mix_img(XS, blk, mx[0], lane);
-        const f32x16 dp = th2_mix_img(XG, blk, mx[2 * 64], lane);
+    constexpr int G = 2;   // blocks (keys) per group: independent chains issued together
+    for (int b0 = w; b0 < 32; b0 += G * H) {
+      f32x16 p[G], dp[G];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) p[r] = ex2(p[r] * kLog2e - lse2[r]);
+      for (int u = 0; u < G; ++u) {
+        p[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, mx[0], lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, mx[2 * 64], lane);
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int blk = b0 + u * H;   // blk = key of this block
+        const bool ok = kb * 32 + blk < a.Nk;   // keys past the end: P2 = dS = 0
         f32x16 ds1;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) ds1[r] = p[r] * (dp[r] - dl[r]);
-#pragma unroll
-        for (int r = 8; r < 16; ++r) {
-          p[r] = 0.f;
-          ds1[r] = 0.f;
+        for (int r = 0; r < NR; ++r) {
+          p[u][r] = ok ? ex2(__builtin_fmaf(p[u][r], kLog2e, -lse2[r])) : 0.f;
+          ds1[r] = p[u][r] * (dp[u][r] - dl[r]);
         }
-        p2 = th2_mix_acc(p, mx[64]);
-        ds = th2_mix_acc(ds1, mx[3 * 64]);
-      } else {
-        p2 = zero16();
-        ds = zero16();
+        if constexpr (!KST) {
+#pragma unroll
+          for (int r = 8; r < 16; ++r) {
+            p[u][r] = 0.f;
+            ds1[r] = 0.f;
+          }
+        }
+        if (blk < 32) {
+          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(p[u], mx[64]), H, lane);     // P2_h over S_h at this key
+          th2_put_block<NR>(XG, blk, th2_mix_acc<KST>(ds1, mx[3 * 64]), H, lane);  // dS_h over dP2_h
+        }
       }
-      th2_put_block(XS, blk, p2, H, lane);   // P2_h over S_h at this key
-      th2_put_block(XG, blk, ds, H, lane);   // dS_h over dP2_h
     }
     __syncthreads();
 #pragma unroll
@@ -645,9 +767,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 }
 
 // LDS: two exchange images + per-wave 32-row staging (two per wave in th2_bwd_kv at <= 8 waves)
-template <int DP> constexpr size_t th2_lds_bytes(int H) { return 2 * (size_t)kTh2Img + (size_t)H * Img<__bf16, DP>::bytes(32); }
-template <int DP> constexpr size_t th2_kv_lds_bytes(int H, bool two_buffers) {
-  return 2 * (size_t)kTh2Img + kTh2MixTbl + (size_t)(two_buffers ? 16 : H) * Img<__bf16, DP>::bytes(32);
+template <int DP, bool KST> constexpr size_t th2_lds_bytes(int H) {
+  return 2 * (size_t)th2_img<KST>() + (size_t)H * Img<__bf16, DP>::bytes(32);
+}
+
+template <int DP, bool KST> constexpr size_t th2_kv_lds_bytes(int H, bool two_buffers) {
+  return 2 * (size_t)th2_img<KST>() + kTh2MixTbl + (size_t)(two_buffers ? 16 : H) * Img<__bf16, DP>::bytes(32);
 }
 
 }  // namespace sae

@@ -1,10 +1,16 @@
-"""CaiT caller on the GPU (models/cait.py): logits shape like the reference's cait_test.py, the bf16
-model against the same model in fp32 (fp32 kernels, checked against the oracle in
-test_gpu_variants.py), and the HIP-graph training step with stochastic depth on."""
+"""CaiT caller on the GPU (models/cait.py): logits shape like the reference's cait_test.py, the
+forward against the float64 oracle (oracle/cait_ref.py: the whole composition -- patch embed,
+talking-heads trunk with LayerScale, class attention over [cls, x], final norm and head) for the
+fp32 and the bf16 model, the bf16 gradients against the fp32 model's (whose kernels are pinned to
+the oracle op by op in test_gpu_variants.py), and the HIP-graph training step with stochastic
+depth on."""
 import copy
 
+import numpy as np
 import pytest
 import torch
+
+import cait_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -29,6 +35,21 @@ def test_cait_logits_shape(dev):
     x = torch.randn(2, 224, 224, 3, device=dev)
     y = m(x, is_training=False)
     assert y.shape == (2, 1000)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_cait_forward_matches_oracle(dev, dtype, tol):
+    m = _small(dtype, dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(4, 64, 64, 3, device=dev, generator=g)
+    with torch.no_grad():
+        y = m(x, is_training=False).double().cpu().numpy()
+    P = {n: p.detach().double().cpu().numpy() for n, p in m.named_parameters()}
+    xin = x.to(dtype).double().cpu().numpy()       # the images as the model sees them
+    ref = cait_ref.cait_forward(P, xin, num_layers=2, num_layers_token_only=2, patch=16)
+    err = float(np.abs(y - ref).max() / np.abs(ref).max())
+    print(f"cait {dtype}: max rel err {err:.2e}")
+    assert err <= tol
 
 
 def test_cait_bf16_matches_fp32(dev):
