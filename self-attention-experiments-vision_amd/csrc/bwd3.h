@@ -127,10 +127,11 @@ template <int DP, int NW> struct B3Stage {
 // the scheduler two independent MFMA / exp chains; KPW = 1 (eight waves, two per SIMD).
 // ROT: q / k rotated as they are staged (the K fragments also feed the K image, so dQ uses the
 // rotated K as it must), dq / dk rotated back as they are stored.
-template <int DP, int NW, int KPW, bool ROT = false>
+// NSU: the 16-wide k-steps of S / dP that carry head-dim columns (3 for D = 48 at DP = 64)
+template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16>
 __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void attn_bwd3_kernel(AttnArgs a) {
   using C = B3<DP, NW, KPW>;
-  constexpr int NS = C::NS, NT = C::NT, BK = C::BK, TB = C::TB, KS = C::KS;
+  constexpr int NS = NSU, NT = C::NT, BK = C::BK, TB = C::TB, KS = C::KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const dsb = smem + 2 * TB;   // two dS^T images (the K image during the prologue)
 

@@ -162,13 +162,14 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 };
 
 // lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false> int fwd2_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16>
+int fwd2_run(hipStream_t st, const AttnArgs& a) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   const long long grid = (long long)nqb * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
   const size_t lds = 4 * (size_t)F2<DP>::TILE;
-  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
   return check_launch("attn_fwd2");
 }
 
@@ -201,6 +202,9 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
   if constexpr (DP <= 64)
     if (a.Nk >= 512) return fwd2_run<DP, 4, 3, false, ROT>(st, a);
   (void)var;
+  // head_dim 48 (CaiT) in 64-wide tiles: QK^T skips the all-zero fourth k-step
+  if constexpr (DP == 64 && !ROT)
+    if (a.D <= 48) return fwd2_run<DP, 4, 2, true, false, 3>(st, a);
   return fwd2_run<DP, 4, 2, true, ROT>(st, a);
 }
 
@@ -230,14 +234,14 @@ template <int DP, bool ROT = false> int bwd2_run_default(hipStream_t st, const A
 // (8 waves x 32 keys, two waves per SIMD); longer key ranges take the two-pass bwd2
 constexpr int kB3Keys = 256;
 
-template <int DP, int NW, int KPW, bool ROT = false> int bwd3_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16> int bwd3_run(hipStream_t st, const AttnArgs& a) {
   using C = B3<DP, NW, KPW>;
   static_assert(C::BK == kB3Keys, "bwd3 dispatch assumes 256-key blocks");
   const long long grid = (long long)a.H * a.B;
   if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3: %d keys > %d", a.Nk, C::BK);
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT>, C::LDS)) return rc;
-  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
+  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>, C::LDS)) return rc;
+  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
   return check_launch("attn_bwd3");
 }
 
@@ -619,6 +623,7 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
       }
 #endif
       if (dp == 32) return bwd3_run<32, 8, 1>(st, a);
+      if (dp == 64 && d->head_dim <= 48) return bwd3_run<64, 8, 1, false, 3>(st, a);   // CaiT head_dim 48
       if (dp == 64) return bwd3_run<64, 8, 1>(st, a);
     }
     if (dp == 32) return bwd2_run_default<32>(st, a);

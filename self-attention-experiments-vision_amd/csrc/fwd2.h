@@ -78,11 +78,13 @@ struct F2Stage {
   }
 };
 
-template <int DP, int NW, bool LSUM, bool FIRST>
+// NSU: the 16-wide k-steps of QK^T that carry head-dim columns (3 for D = 48 at DP = 64: the
+// fourth would multiply zero padding)
+template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS>
 __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
                                           f32x16& lacc, float& m, float& l, int nvalid, float sl2,
                                           const unsigned* ka, const unsigned* va, int h) {
-  constexpr int NS = F2<DP>::NS, NT = F2<DP>::NT;
+  constexpr int NS = NSU, NT = F2<DP>::NT;
   // nvalid: keys of this tile that exist (64 for every tile but the tail)
   const bool two = nvalid > 32;
   f32x16 s0 = zero16(), s1 = zero16();
@@ -188,10 +190,10 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 
 // ROT: q and k are rotated (rotary, common.h rope8) as they are staged -- q fragments once, each
 // K tile as it goes to LDS -- so the rotated tensors never exist in HBM.
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false>
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   using FF = F2<DP>;
-  constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
+  constexpr int NS = NSU, NT = FF::NT, TILE = FF::TILE;
   constexpr int BQ = 32 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       vst.load(rv, (unsigned)(t + 1) * vstep);
     }
     if constexpr (decltype(compute_c)::value)
-      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value>(cur, cur + TILE, qf, acco, lacc, m, l,
+      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU>(cur, cur + TILE, qf, acco, lacc, m, l,
                                                         min(64, a.Nk - 64 * t), sl2, ka, va, h);
     if (t + 1 < nkt) {
       if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);

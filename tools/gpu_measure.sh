@@ -1,9 +1,15 @@
+#!/bin/bash
+# One-box measurement of a round (run on the GPU box from the repo root):
+#   bench JSON, rocprofv3 kernel stats of the SAME build (training loop and attention bench),
+#   PMC passes for the DeiT-S training step and the ViT-B@384 attention headline.
+# usage: tools/gpu_measure.sh <tag>     -> gpurun_out/<tag>_*
 set -e
+tag=${1:-r02}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train -o run -- python3 bench.py --profile --steps 5 --warmup 3 > gpurun_out/prof_train.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_attn -o run -- python3 tools/attn_bench.py --iters 10 > gpurun_out/prof_attn.log 2>&1
-tools/pmc.sh gpurun_out/pmc_train python3 bench.py --profile --eager --steps 3 --warmup 2
-tools/pmc.sh gpurun_out/pmc_b384 python3 tools/attn_bench.py --shapes vitb384 --iters 3
+timeout -k 10 400 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_train -o run -- python3 bench.py --profile --steps 5 --warmup 3 > gpurun_out/${tag}_prof_train.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof_attn -o run -- python3 tools/attn_bench.py --iters 10 > gpurun_out/${tag}_prof_attn.log 2>&1
+tools/pmc.sh gpurun_out/${tag}_pmc_train python3 bench.py --profile --eager --steps 3 --warmup 2
+tools/pmc.sh gpurun_out/${tag}_pmc_b384 python3 tools/attn_bench.py --shapes vitb384 --iters 3
 echo ALL_DONE
