@@ -70,6 +70,8 @@ class TrainStep:
         self.model = model
         params = [p for p in model.parameters() if p.requires_grad]
         self._params = params
+        if self.world > 1:
+            self._broadcast_from_rank0([t for t in model.state_dict().values() if torch.is_tensor(t)])
         # flat_grads (default: world > 1) selects the multi-rank step structure: flat gradient
         # buffer + two graphs around the all-reduce (settable at world 1 to test that structure)
         self.flat = self.world > 1 if flat_grads is None else bool(flat_grads)
@@ -102,6 +104,28 @@ class TrainStep:
         except (RuntimeError, TypeError):
             self.opt = torch.optim.AdamW(params, foreach=True, **kw)
         self.smoothing = label_smoothing
+
+    @staticmethod
+    def _broadcast_from_rank0(tensors):
+        """Once, at construction: every replica starts from rank 0's parameters and buffers (the
+        reference's pmap replicates one host-initialised state, train.py:226-228), whatever seed
+        each rank used.  One flat broadcast per dtype, not one per tensor."""
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for ts in by_dtype.values():
+            flat = torch.cat([t.detach().reshape(-1) for t in ts])
+            if flat.is_cuda and dist.get_backend() == "gloo":
+                host = flat.cpu()
+                dist.broadcast(host, src=0)
+                flat.copy_(host)
+            else:
+                dist.broadcast(flat, src=0)
+            off = 0
+            with torch.no_grad():
+                for t in ts:
+                    t.copy_(flat[off:off + t.numel()].view_as(t))
+                    off += t.numel()
 
     # ---- pieces of one step
     def _zero_grad(self):

@@ -3,7 +3,8 @@
 The training step (sae_vision_amd.train.TrainStep, the rebuild of the reference's
 pmap(train_step) + lax.pmean(grads), train.py:94-96,230: flat gradient buffer, bucketed SUM
 all-reduce of the gradients of loss / world) must give every rank the same parameters as a
-single process stepping on the concatenated global batch (global-mean gradient, survey D9).
+single process stepping on the concatenated global batch (global-mean gradient, survey D9),
+starting from rank 0's initial state whatever the other ranks initialised.
 The GPU step runs the same code between its two HIP graphs.  The attention kernels themselves are replicas (GPU only); this checks the
 collective / bucketing / optimizer path with a small CPU model.
 """
@@ -17,9 +18,9 @@ import torch.multiprocessing as mp
 
 
 class TinyNet(torch.nn.Module):
-    def __init__(self):
+    def __init__(self, seed: int = 0):
         super().__init__()
-        torch.manual_seed(0)
+        torch.manual_seed(seed)
         self.l1 = torch.nn.Linear(12, 16)
         self.l2 = torch.nn.Linear(16, 5)
 
@@ -41,7 +42,8 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x, y = _data()
     per = x.shape[0] // world
-    step = train.TrainStep(TinyNet(), global_batch=x.shape[0], bucket_cap_mb=0.0001)
+    # each rank initialises from its own seed: the step broadcasts rank 0's state at construction
+    step = train.TrainStep(TinyNet(seed=rank), global_batch=x.shape[0], bucket_cap_mb=0.0001)
     # the flat gradient buffer: every .grad a view into it, buckets tile it from the end (the
     # order the backward completes the parameters), each at least the cap unless it is the last
     n = sum(p.numel() for p in step.model.parameters())
