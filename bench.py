@@ -20,7 +20,9 @@ Rank 0 prints ONE JSON line:
                  (DESIGN.md §4);
                  traffic = HBM bytes per call from profiles/pmc_traffic.json (rocprofv3 PMC)
   cpu_baseline = the numpy port (oracle/vit_ref.py) of the same training step on a bounded
-                 sample, on this host's cores (rank 0, N=1 only)
+                 sample, on this host's cores (rank 0, N=1 only); .configs0 = BASELINE configs[0]
+                 (DeiT-Ti forward + loss, batch 8); .attention = the unfused attention core fwd+bwd
+                 as C + OpenMP (oracle/attn_cpu.c), TFLOP/s
   attention_headline = the fused fwd+bwd core alone at ViT-B/16@384 shape (B=64, N=577, H=12,
                  D=64), TFLOP/s and fraction of the 2.5 PF bf16 MFMA peak (N>=577 target), timed
                  on HIP graphs of back-to-back launches (no host gaps)
@@ -130,7 +132,32 @@ def cpu_baseline(model_name, seconds_budget=15.0):
     out["configs0"] = {"value": round(8 / d1, 3), "unit": "img/s", "ms_per_batch": round(d1 * 1e3, 1),
                        "cores": int(cores), "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
                        "sample": f"deit_ti_patch16 224px fp32 numpy forward+loss, batch 8 x {n}"}
+    out["attention"] = cpu_attention_baseline(seconds_budget / 3)
     return out
+
+
+def cpu_attention_baseline(seconds_budget=5.0, B=16, N=197, H=6, D=64):
+    """SURVEY §8d's CPU baseline of metric (1): the unfused reference attention core (S and P
+    materialised, softmax, AV; backward through dP / dS) as C + OpenMP over (batch, head), fp32
+    (oracle/attn_cpu.c), fwd + bwd on a DeiT-S-shaped sample, TFLOP/s by the same algorithmic count
+    as the GPU line (12 B H N^2 D)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import attn_cpu
+    rng = np.random.default_rng(0)
+    q, k, v, do = (rng.standard_normal((B, N, H, D)).astype(np.float32) for _ in range(4))
+    o, lse = attn_cpu.attn_fwd(q, k, v)   # warm-up (thread pool, page faults)
+    n, t0 = 0, time.perf_counter()
+    while n < 1 or time.perf_counter() - t0 < seconds_budget:
+        o, lse = attn_cpu.attn_fwd(q, k, v)
+        attn_cpu.attn_bwd(q, k, v, o, lse, do)
+        n += 1
+    dt = (time.perf_counter() - t0) / n
+    f_fwd, f_bwd, _, _ = attn_work(B, N, N, H, D)
+    return {"value": round((f_fwd + f_bwd) / dt / 1e12, 5), "unit": "TFLOP/s", "ms_per_call": round(dt * 1e3, 2),
+            "cores": attn_cpu.threads(), "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
+            "sample": f"unfused fp32 attention core fwd+bwd (C + OpenMP, oracle/attn_cpu.c), B={B} N={N} H={H} "
+                      f"D={D}, {n} calls"}
 
 
 def headline(dev, iters=20, reps=10, f32=False):
