@@ -20,7 +20,11 @@ namespace sae {
 // dK/dV pass.  Per 32-key half: S^T = K Q^T, dP^T = V dO^T (row reads of the K / V images),
 // dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T (transposed reads of the K image).
 // ROT (both passes): q / k rotated as they are staged, dq / dk rotated back as they are stored.
-template <int DP, int NW, int MINW, bool ROT = false>
+// REL (both passes): the BoTNet relative logits enter the recomputed scores as two extra k-steps
+// (fwd2.h rel_onehot8 / rel_qrow8); the dQ pass also forms dbias^T = onehot^T dS^T on the matrix
+// pipe -- one more 32 x 32 accumulator, complete per query row because the pass sweeps every key
+// -- and stores dbias_h / dbias_w (deterministic, no atomics).
+template <int DP, int NW, int MINW, bool ROT = false, bool REL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -119,10 +123,29 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
     }
   }
   f32x16 adq[NT];   // written first by the peeled first tile (zero C operand)
+  // REL: query-bias fragments, one-hot row reads (scores) and transposed reads (dbias^T)
+  char* const rimg = smem + 4 * TILE;
+  bf16x8 qa[2];
+  unsigned rra[2], rca[2];
+  f32x16 adb = zero16();
+  if constexpr (REL) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qa[s] = __builtin_bit_cast(bf16x8, rel_qrow8(a, rowoff + q, qok, 2 * s + h, 1.f / a.scale));
+      rra[s] = r32 * 64 + 16 * ((2 * s + h) ^ swz<32>(r32));
+    }
+    const int li = lane & 15, g = lane >> 4;
+    const int colb = 16 * (g & 1) + 4 * (li & 3);
+    const int chunk = colb >> 3, half = (colb >> 2) & 1;
+    const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+    rca[0] = r1 * 64 + 16 * (chunk ^ swz<32>(r1)) + 8 * half;
+    rca[1] = r2 * 64 + 16 * (chunk ^ swz<32>(r2)) + 8 * half;
+  }
 
   if constexpr (ROT) kst.rope(a.rope, 0, tid);
   kst.write(smem);
   vst.write(smem + TILE);
+  if constexpr (REL) rel_put_onehot<NW>(a, rimg, 0, tid);
   vm_wait_all();   // Q / dO fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1, barrier (as fwd2.h)
@@ -131,6 +154,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
     constexpr bool FIRST = decltype(first_c)::value;
     const char* ldsK = smem + bsel * 2 * TILE;
     const char* ldsV = ldsK + TILE;
+    const char* ldsR = rimg + bsel * kRelImg;
     char* nxt = smem + (bsel ^ 1) * 2 * TILE;
     if (t + 1 < nkt) {
       kst.load(rk, (unsigned)(t + 1) * kstep);
@@ -149,6 +173,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
           const bf16x8 vr = *reinterpret_cast<const bf16x8*>(ldsV + ka[s] + 32 * u * DP * 2);
           sp = MF<__bf16>::mma(kr, qf[s], sp);
           dp = MF<__bf16>::mma(vr, gf[s], dp);
+        }
+        if constexpr (REL) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            sp = MF<__bf16>::mma(*reinterpret_cast<const bf16x8*>(ldsR + rra[s] + 32 * u * 64), qa[s], sp);
         }
         if (nvalid < 64) {   // tail: keys past the end contribute nothing
           const int nvh = nvalid - 32 * u - 4 * h;
@@ -170,6 +199,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
             adq[tt] = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, vv), sf,
                                       (FIRST && u == 0 && s2 == 0) ? zero16() : adq[tt]);
           }
+          if constexpr (REL) {   // dbias^T += onehot^T dS^T (the one-hot image read transposed)
+            const int ro = (32 * u + 16 * s2) * 64;
+            s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsR + rca[0] + ro));
+            s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ldsR + rca[1] + ro));
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x8 ov = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+            adb = MF<__bf16>::mma(__builtin_bit_cast(bf16x8, ov), sf, adb);
+          }
         }
       }
     }
@@ -177,6 +214,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);
       kst.write(nxt);
       vst.write(nxt + TILE);
+      if constexpr (REL) rel_put_onehot<NW>(a, rimg + (bsel ^ 1) * kRelImg, 64 * (t + 1), tid);
     }
     __syncthreads();
   };
@@ -191,6 +229,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   };
   if (active) sweep(std::true_type{});   // waves past the last query row only stage and sync
   else sweep(std::false_type{});
+  if constexpr (REL) {   // dbias^T: accumulator row = table column row_of(r, h), lane = query
+    if (active && qok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int col = row_of(r, h);
+        if (col < a.rel_h) a.dbias_h[(rowoff + q) * a.rel_h + col] = adb[r];
+        else if (col < a.rel_h + a.rel_w) a.dbias_w[(rowoff + q) * a.rel_w + col - a.rel_h] = adb[r];
+      }
+    }
+  }
   if (active) {
     const int q0 = qb * BQ + w * 32;
     __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
@@ -204,12 +252,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
 // each 64-query Q / dO tile and its row constants (lse * log2 e, delta).  Per 32-query half:
 // S = Q K^T, dP = dO V^T (row reads), P = 2^(S sl2 - lse2), dS = P o (dP - delta),
 // dV^T += dO^T P and dK^T += Q^T dS (transposed reads of the dO / Q images).
-template <int DP, int NW, int MINW, bool ROT = false>
+// REL: the staged tile also carries the query-bias rows of its 64 queries ([64][32] bf16 image),
+// the wave's keys hold their one-hot rows in registers.
+template <int DP, int NW, int MINW, bool ROT = false, bool REL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
   constexpr int BK = 32 * NW;
-  constexpr int TB = 2 * TILE + 2 * 64 * 4;   // [Q img | dO img | lse2[64] | delta[64]]
+  // [Q img | dO img | lse2[64] | delta[64] (| query-bias img)]
+  constexpr int TB = 2 * TILE + 2 * 64 * 4 + (REL ? kRelImg : 0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nkb = (a.Nk + BK - 1) / BK;
@@ -240,6 +291,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   const unsigned qstep = (unsigned)(64 * a.qs[1] * 2), gstep = (unsigned)(64 * a.dos[1] * 2);
   const int nqt = (a.Nq + 63) / 64;
   float rc_l[2] = {0.f, 0.f}, rc_d[2] = {0.f, 0.f};   // row constants of a staged tile (threads 0..63)
+  uint4 rq8[2];   // REL: this thread's query-bias chunk of a staged tile (threads 0..255)
   auto fetch = [&](int r, int qt) {
     qst[r].load(rq, (unsigned)qt * qstep);
     gst[r].load(rg, (unsigned)qt * gstep);
@@ -247,6 +299,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
       const int qq = qt * 64 + tid;
       rc_l[r] = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
       rc_d[r] = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+    }
+    if constexpr (REL) {
+      static_assert(NW == 4, "REL staging: one query-bias chunk per thread");
+      const int qq = qt * 64 + (tid >> 2);
+      rq8[r] = rel_qrow8(a, rowoff + qq, qq < a.Nq, tid & 3, 1.f / a.scale);
     }
   };
   fetch(0, 0);
@@ -268,6 +325,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     if constexpr (ROT) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) kf[s] = rope8<1>(kf[s], a.rope, key, 16 * s + 8 * h);
+    }
+  }
+  // REL: the one-hot row of this lane's key (B operand) and the query-bias image row reads
+  bf16x8 kfa[2];
+  unsigned rra[2];
+  if constexpr (REL) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kfa[s] = __builtin_bit_cast(bf16x8, rel_onehot8(a, key, 2 * s + h));
+      rra[s] = r32 * 64 + 16 * ((2 * s + h) ^ swz<32>(r32));
     }
   }
   const float sl2 = a.scale * kLog2e;
@@ -300,6 +367,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     if (tid < 64) {
       reinterpret_cast<float*>(buf + 2 * TILE)[tid] = rc_l[r];
       reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d[r];
+    }
+    if constexpr (REL) {
+      const int rr = tid >> 2, c = tid & 3;
+      *reinterpret_cast<uint4*>(buf + 2 * TILE + 512 + rr * 64 + 16 * (c ^ swz<32>(rr))) = rq8[r];
     }
   };
   put(0, smem, 0);
@@ -338,6 +409,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
           const bf16x8 gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
           sp = MF<__bf16>::mma(qr, kf[s], sp);
           dp = MF<__bf16>::mma(gr, vf[s], dp);
+        }
+        if constexpr (REL) {
+          const char* ldsR = ldsQ + 2 * TILE + 512;
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            sp = MF<__bf16>::mma(*reinterpret_cast<const bf16x8*>(ldsR + rra[s] + 32 * u * 64), kfa[s], sp);
         }
         // rows q = 32u + row_of(r, h): constants for r = 4g + j at 32u + 8g + 4h + j
 #pragma unroll

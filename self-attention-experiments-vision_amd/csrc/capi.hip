@@ -162,16 +162,21 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 };
 
 // lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16>
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false>
 int fwd2_run(hipStream_t st, const AttnArgs& a) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   const long long grid = (long long)nqb * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  const size_t lds = 4 * (size_t)F2<DP>::TILE;
-  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), lds, st, a);
+  const size_t lds = 4 * (size_t)F2<DP>::TILE + (REL ? 2 * kRelImg : 0);
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL>), dim3((unsigned)grid), dim3(64 * NW), lds,
+                     st, a);
   return check_launch("attn_fwd2");
 }
+
+// BoTNet relative logits on the lean bf16 kernels: the table columns (Hs + Ws) fit the two extra
+// score k-steps; larger grids (up to 64 x 64) and fp32 take the v1 kernels
+static bool rel_lean(const AttnArgs& a) { return a.rel_h + a.rel_w <= kRelCols; }
 
 // Development A/B knobs (schedule variants picked by environment variable) exist only in the
 // debug build (build.py --dev defines SAE_DEV_KNOBS); the release library takes the fixed
@@ -209,20 +214,23 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
 }
 
 // lean bf16 backward (bwd2.h): dQ pass (publishes delta) then dK/dV pass
-template <int DP, int NWQ, int MQ, int NWK, int MK, bool ROT = false> int bwd2_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NWQ, int MQ, int NWK, int MK, bool ROT = false, bool REL = false>
+int bwd2_run(hipStream_t st, const AttnArgs& a) {
   {
     const long long grid = (long long)((a.Nq + 32 * NWQ - 1) / (32 * NWQ)) * a.H * a.B;
     if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-    const size_t lds = 4 * (size_t)F2<DP>::TILE;
-    if (int rc = lds_attr((const void*)attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT>, lds)) return rc;
-    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT>), dim3((unsigned)grid), dim3(64 * NWQ), lds, st, a);
+    const size_t lds = 4 * (size_t)F2<DP>::TILE + (REL ? 2 * kRelImg : 0);
+    if (int rc = lds_attr((const void*)attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT, REL>, lds)) return rc;
+    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, NWQ, MQ, ROT, REL>), dim3((unsigned)grid), dim3(64 * NWQ), lds, st,
+                       a);
     if (int rc = check_launch("attn_bwd2_dq")) return rc;
   }
   const long long grid = (long long)((a.Nk + 32 * NWK - 1) / (32 * NWK)) * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512);
-  if (int rc = lds_attr((const void*)attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT>, lds)) return rc;
-  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT>), dim3((unsigned)grid), dim3(64 * NWK), lds, st, a);
+  const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512 + (REL ? kRelImg : 0));
+  if (int rc = lds_attr((const void*)attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT, REL>, lds)) return rc;
+  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, NWK, MK, ROT, REL>), dim3((unsigned)grid), dim3(64 * NWK), lds, st,
+                     a);
   return check_launch("attn_bwd2_dkdv");
 }
 
@@ -532,6 +540,13 @@ static int attn_fwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     if (dp == 64) return fwd2_dispatch<64>((hipStream_t)stream, a, var);
     if (dp == 128) return fwd2_dispatch<128>((hipStream_t)stream, a, var);
   }
+  if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && rel && rel_lean(a)) {   // BoTNet
+    const int dp = pick_dp(d->head_dim);
+    hipStream_t st = (hipStream_t)stream;
+    if (dp == 32) return fwd2_run<32, 4, 2, true, false, 2, true>(st, a);
+    if (dp == 64) return fwd2_run<64, 4, 2, true, false, 4, true>(st, a);
+    return fwd2_run<128, 4, 2, true, false, 8, true>(st, a);
+  }
   return dispatch<FwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }
 
@@ -614,8 +629,7 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;
-    // head_dim 128 (BoTNet) stays on the v1 kernels (register budget of the lean passes)
-    if (a.Nk <= kB3Keys && var != 2) {
+    if (a.Nk <= kB3Keys && var != 2 && dp <= 64) {
 #ifdef SAE_DEV_KNOBS
       if (var == 3) {   // four waves x two 32-key sub-blocks (one wave per SIMD): measured slower
         if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
@@ -628,6 +642,16 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     }
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);
+    // head_dim 128 (BoTNet): one wave per SIMD (the dK / dV accumulators of 32 keys x 128 columns
+    // plus the K / V fragments need more than half the register file)
+    return bwd2_run<128, 4, 1, 4, 1>(st, a);
+  }
+  if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && rel && rel_lean(a)) {   // BoTNet relative logits
+    const int dp = pick_dp(d->head_dim);
+    hipStream_t st = (hipStream_t)stream;
+    if (dp == 32) return bwd2_run<32, 4, 2, 4, 2, false, true>(st, a);
+    if (dp == 64) return bwd2_run<64, 4, 2, 4, 1, false, true>(st, a);
+    return bwd2_run<128, 4, 2, 4, 1, false, true>(st, a);
   }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
 }

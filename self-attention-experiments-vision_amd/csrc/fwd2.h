@@ -40,6 +40,59 @@ __device__ __forceinline__ float xhalf_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// BoTNet relative logits on the matrix pipe (REL, botnet.py:191-192 in the index-map form of
+// sae_attn.h): bias_h[q][k / Ws] + bias_w[q][k % Ws] is the dot product of a per-query row
+// [bias_h[q][0 .. Hs) | bias_w[q][0 .. Ws) | 0] / scale (bf16) with a per-key one-hot row (1 at
+// k / Ws and at Hs + k % Ws), i.e. two more 16-deep k-steps of the score MFMA (Hs + Ws <= 32) in
+// place of two gathers and two adds per score on the VALU.  The one-hot rows of a 64-key tile
+// are a [64][32] bf16 image (64-byte rows, swz<32>) generated while the tile is staged; the
+// dQ pass also reads it transposed, as the A operand of dbias^T = onehot^T dS^T.
+constexpr int kRelCols = 32;
+constexpr int kRelImg = 64 * kRelCols * 2;
+
+// one-hot row of `key`, columns 8c .. 8c + 7 (zero past Nk)
+__device__ __forceinline__ uint4 rel_onehot8(const AttnArgs& a, int key, int c) {
+  unsigned m = 0;
+  if (key < a.Nk) {
+    const int kx = (key * a.rel_magic) >> 20;
+    m = (1u << kx) | (1u << (a.rel_h + key - kx * a.rel_w));
+  }
+  const unsigned b = m >> (8 * c);
+  uint4 r;
+  r.x = ((b & 1u) ? 0x3F80u : 0u) | ((b & 2u) ? 0x3F800000u : 0u);
+  r.y = ((b & 4u) ? 0x3F80u : 0u) | ((b & 8u) ? 0x3F800000u : 0u);
+  r.z = ((b & 16u) ? 0x3F80u : 0u) | ((b & 32u) ? 0x3F800000u : 0u);
+  r.w = ((b & 64u) ? 0x3F80u : 0u) | ((b & 128u) ? 0x3F800000u : 0u);
+  return r;
+}
+
+// query-bias row of score row `row` = (b H + h) Nq + q, columns 8c .. 8c + 7, times inv (1 / scale)
+__device__ __forceinline__ uint4 rel_qrow8(const AttnArgs& a, size_t row, bool ok, int c, float inv) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = 8 * c + j;
+    float v = 0.f;
+    if (ok && col < a.rel_h) v = a.bias_h[row * a.rel_h + col];
+    else if (ok && col < a.rel_h + a.rel_w) v = a.bias_w[row * a.rel_w + col - a.rel_h];
+    r[j] = (__bf16)(v * inv);
+  }
+  return __builtin_bit_cast(uint4, r);
+}
+
+// the one-hot image of keys key0 .. key0 + 63 (threads 0 .. 255 one 16-byte chunk each)
+template <int NW>
+__device__ __forceinline__ void rel_put_onehot(const AttnArgs& a, char* img, int key0, int tid) {
+#pragma unroll
+  for (int i = 0; i < (256 + 64 * NW - 1) / (64 * NW); ++i) {
+    const int id = tid + 64 * NW * i;
+    if (256 % (64 * NW) == 0 || id < 256) {
+      const int r = id >> 2, c = id & 3;
+      *reinterpret_cast<uint4*>(img + r * 64 + 16 * (c ^ swz<32>(r))) = rel_onehot8(a, key0 + r, c);
+    }
+  }
+}
+
 template <int DP, int NW>
 struct F2Stage {
   static constexpr int NCH = (64 * F2<DP>::CPR + 64 * NW - 1) / (64 * NW);
@@ -80,10 +133,13 @@ struct F2Stage {
 
 // NSU: the 16-wide k-steps of QK^T that carry head-dim columns (3 for D = 48 at DP = 64: the
 // fourth would multiply zero padding)
-template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS>
+// REL: ldsR = the tile's one-hot image, ra = this lane's row reads of it, qa = query-bias rows
+template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS, bool REL = false>
 __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
                                           f32x16& lacc, float& m, float& l, int nvalid, float sl2,
-                                          const unsigned* ka, const unsigned* va, int h) {
+                                          const unsigned* ka, const unsigned* va, int h,
+                                          const char* ldsR = nullptr, const unsigned* ra = nullptr,
+                                          const bf16x8* qa = nullptr) {
   constexpr int NS = NSU, NT = F2<DP>::NT;
   // nvalid: keys of this tile that exist (64 for every tile but the tail)
   const bool two = nvalid > 32;
@@ -93,11 +149,20 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
     const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ldsK + ka[s]);
     s0 = MF<__bf16>::mma(k0, qf[s], s0);
   }
+  if constexpr (REL) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) s0 = MF<__bf16>::mma(*reinterpret_cast<const bf16x8*>(ldsR + ra[s]), qa[s], s0);
+  }
   if (two) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ldsK + ka[s] + 32 * DP * 2);
       s1 = MF<__bf16>::mma(k1, qf[s], s1);
+    }
+    if constexpr (REL) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        s1 = MF<__bf16>::mma(*reinterpret_cast<const bf16x8*>(ldsR + ra[s] + 32 * 64), qa[s], s1);
     }
   }
   if (nvalid < 64) {   // tail tile: keys past the end score -inf (key = row_of(r, h) = c_r + 4h)
@@ -190,7 +255,9 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 
 // ROT: q and k are rotated (rotary, common.h rope8) as they are staged -- q fragments once, each
 // K tile as it goes to LDS -- so the rotated tensors never exist in HBM.
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16>
+// REL: BoTNet relative logits as two extra score k-steps (rel_onehot8 / rel_qrow8 above); the
+// one-hot images follow the K / V buffers in LDS.
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = NSU, NT = FF::NT, TILE = FF::TILE;
@@ -238,6 +305,18 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       for (int s = 0; s < NS; ++s) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
     }
   }
+  // REL: query-bias fragments (columns 16s + 8h .. + 7) and the one-hot row reads
+  bf16x8 qa[2];
+  unsigned ra[2];
+  if constexpr (REL) {
+    const size_t row = ((size_t)b * a.H + hh) * a.Nq + q;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qa[s] = __builtin_bit_cast(bf16x8, rel_qrow8(a, row, q < a.Nq, 2 * s + h, 1.f / a.scale));
+      ra[s] = r32 * 64 + 16 * ((2 * s + h) ^ swz<32>(r32));
+    }
+  }
+  char* const rimg = smem + 4 * TILE;   // REL: two one-hot images
   // per-lane LDS read addresses: K rows r32 (+32 as an immediate), V^T transposed reads
   unsigned ka[NS], va[2 * NT];
 #pragma unroll
@@ -261,6 +340,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   if constexpr (ROT) kst.rope(a.rope, 0, tid);
   kst.write(smem);
   vst.write(smem + TILE);
+  if constexpr (REL) rel_put_onehot<NW>(a, rimg, 0, tid);
   vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
   __syncthreads();
   // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1 into the other
@@ -275,12 +355,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       vst.load(rv, (unsigned)(t + 1) * vstep);
     }
     if constexpr (decltype(compute_c)::value)
-      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU>(cur, cur + TILE, qf, acco, lacc, m, l,
-                                                        min(64, a.Nk - 64 * t), sl2, ka, va, h);
+      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU, REL>(cur, cur + TILE, qf, acco, lacc, m, l,
+                                                             min(64, a.Nk - 64 * t), sl2, ka, va, h,
+                                                             rimg + bsel * kRelImg, ra, qa);
     if (t + 1 < nkt) {
       if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);
       kst.write(nxt);
       vst.write(nxt + TILE);
+      if constexpr (REL) rel_put_onehot<NW>(a, rimg + (bsel ^ 1) * kRelImg, 64 * (t + 1), tid);
     }
     __syncthreads();
   };

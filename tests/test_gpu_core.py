@@ -23,6 +23,8 @@ CASES = [
     (2, 196, 196, 8, 48, "f32"),                 # CaiT trunk runs fp32 (survey D7)
     (1, 49, 49, 4, 128, "bf16"),                 # BoTNet 7x7, D = 128
     (1, 49, 49, 4, 128, "f32"),
+    (2, 196, 196, 4, 128, "bf16"),               # BoTNet 14x14, D = 128 (two-pass lean backward)
+    (1, 130, 70, 2, 96, "bf16"),                 # head dim 96 in 128-wide tiles, Nq != Nk
     (3, 16, 16, 4, 10, "f32"),                   # TNT inner attention, D = 10 (scalar path)
     (3, 16, 16, 4, 6, "bf16"),                   # TNT-B inner, D = 6
     (2, 1, 197, 8, 48, "bf16"),                  # CaiT class attention (Nq = 1)

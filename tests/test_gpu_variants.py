@@ -62,7 +62,10 @@ def test_talking_heads(dev, B, N, Nk, H, D, mode):
     (14, 14, 4, 128, "f32"),    # BoTNet 14x14 at its real head dim (BASELINE configs[3])
     (14, 14, 4, 128, "bf16"),
     (14, 14, 4, 16, "f32"),     # 14x14 grid, small D
+    (14, 14, 4, 16, "bf16"),    # lean kernels at 32-wide tiles
     (5, 7, 2, 32, "f32"),       # non-square grid
+    (5, 7, 2, 32, "bf16"),
+    (7, 7, 4, 64, "bf16"),      # lean kernels at 64-wide tiles
 ])
 def test_botnet_relpos(dev, Hs, Ws, H, D, mode):
     import torch

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
     ap.add_argument("--th", action="store_true", help="talking-heads attention (orthogonal T1, T2)")
+    ap.add_argument("--rel", action="store_true",
+                    help="BoTNet relative logits (square Hs = Ws = sqrt(Nk) grid, N(0, 1/D) bias tables)")
     ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B (dev build: SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so)")
     ap.add_argument("--bwd-variants", default="", help="comma list of SAE_BWD_VARIANT values to A/B")
     args = ap.parse_args()
@@ -51,7 +53,7 @@ def main():
     runs = [(n, f, b) for n in args.shapes.split(",") for f in fv for b in bv]
     for shape, fvar, bvar in runs:
         os.environ["SAE_FWD_VARIANT"], os.environ["SAE_BWD_VARIANT"] = fvar, bvar
-        name = shape + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
+        name = shape + ("+rel" if args.rel else "") + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
         B, Nq, Nk, H, D = SHAPES[shape]
         g = torch.Generator(device=dev).manual_seed(0)
         q = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
@@ -65,6 +67,15 @@ def main():
             o, lse, _, _ = ops._th_fwd(q, k, v, th1, th2, sc)
             fwd_call = lambda: ops._th_fwd(q, k, v, th1, th2, sc)
             bwd_call = lambda: ops._th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, sc)
+        elif args.rel:
+            hs = int(round(math.sqrt(Nk)))
+            assert hs * hs == Nk and Nq == Nk, "--rel: square key grid"
+            bh = torch.randn(B, H, Nq, hs, device=dev, generator=g) / math.sqrt(D)
+            bw = torch.randn(B, H, Nq, hs, device=dev, generator=g) / math.sqrt(D)
+            grid = (hs, hs)
+            o, lse = ops._fwd(q, k, v, sc, bh, bw, grid)
+            fwd_call = lambda: ops._fwd(q, k, v, sc, bh, bw, grid)
+            bwd_call = lambda: ops._bwd(q, k, v, o, lse, do, dq, dk, dv, sc, bh, bw, grid)
         else:
             o, lse = ops._fwd(q, k, v, sc)
             fwd_call = lambda: ops._fwd(q, k, v, sc)
