@@ -40,7 +40,7 @@ def build(force=False, debug=False, verbose=True, dev=False):
             print(f"[build] {out} is up to date")
         return out
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-I", os.path.join(ROOT, "include"),
+           "-Wno-unused-function", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"),
            os.path.join(SRC, "capi.hip"), "-o", out + ".tmp"]
     if debug:
         cmd.insert(3, "-g")

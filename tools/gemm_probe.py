@@ -33,6 +33,7 @@ def main():
     M = 128 * 197
     shapes = [  # (name, M, K, N)
         ("qkv", M, 384, 1152), ("oproj", M, 384, 384), ("ff1", M, 384, 1536), ("ff2", M, 1536, 384),
+        ("qkv_dx", M, 1152, 384),
         ("b384_qkv", 32 * 577, 768, 2304), ("b384_ff1", 32 * 577, 768, 3072), ("b384_ff2", 32 * 577, 3072, 768),
     ]
     for name, m, k, n in shapes:
