@@ -131,7 +131,7 @@ template <int DP, int NW> struct B3Stage {
 template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16>
 __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void attn_bwd3_kernel(AttnArgs a) {
   using C = B3<DP, NW, KPW>;
-  constexpr int NS = NSU, NT = C::NT, BK = C::BK, TB = C::TB, KS = C::KS;
+  constexpr int NS = NSU, NT = C::NT, TB = C::TB, KS = C::KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const dsb = smem + 2 * TB;   // two dS^T images (the K image during the prologue)
 

@@ -19,6 +19,7 @@
 #include "fwd2.h"
 #include "bwd2.h"
 #include "bwd3.h"
+#include "cls.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
 #include "patch.h"
@@ -177,6 +178,30 @@ int fwd2_run(hipStream_t st, const AttnArgs& a) {
 // BoTNet relative logits on the lean bf16 kernels: the table columns (Hs + Ws) fit the two extra
 // score k-steps; larger grids (up to 64 x 64) and fp32 take the v1 kernels
 static bool rel_lean(const AttnArgs& a) { return a.rel_h + a.rel_w <= kRelCols; }
+
+// single query row (CaiT class attention, CeiT LCA): the K/V stream kernels of cls.h
+constexpr int kClsMaxKeys = 1 << 20;
+static bool cls_ok(const sae_attn_desc* d) {
+  return d->seq_q == 1 && d->seq_k <= kClsMaxKeys && d->head_dim <= 128 && d->dtype == SAE_DTYPE_BF16 &&
+         !(d->flags & SAE_FLAG_RELPOS);
+}
+template <bool BWD> int cls_run(hipStream_t st, const AttnArgs& a) {
+  const long long grid = (long long)a.B * a.H;
+  if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  const bool two = a.D > 64;
+  const size_t lds = two ? cls_lds_bytes<2>() : cls_lds_bytes<1>();
+  const void* fn = BWD ? (two ? (const void*)attn_cls_bwd_kernel<2> : (const void*)attn_cls_bwd_kernel<1>)
+                       : (two ? (const void*)attn_cls_fwd_kernel<2> : (const void*)attn_cls_fwd_kernel<1>);
+  if (int rc = lds_attr(fn, lds)) return rc;
+  if (BWD) {
+    if (two) hipLaunchKernelGGL(attn_cls_bwd_kernel<2>, dim3((unsigned)grid), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL(attn_cls_bwd_kernel<1>, dim3((unsigned)grid), dim3(256), lds, st, a);
+    return check_launch("attn_cls_bwd");
+  }
+  if (two) hipLaunchKernelGGL(attn_cls_fwd_kernel<2>, dim3((unsigned)grid), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(attn_cls_fwd_kernel<1>, dim3((unsigned)grid), dim3(256), lds, st, a);
+  return check_launch("attn_cls_fwd");
+}
 
 // Development A/B knobs (schedule variants picked by environment variable) exist only in the
 // debug build (build.py --dev defines SAE_DEV_KNOBS); the release library takes the fixed
@@ -534,6 +559,7 @@ static int attn_fwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     if (dp == 64) return fwd2_dispatch<64, true>((hipStream_t)stream, a, 0);
     return fwd2_dispatch<128, true>((hipStream_t)stream, a, 0);
   }
+  if (var != 1 && vec && cls_ok(d)) return cls_run<false>((hipStream_t)stream, a);
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     if (dp == 32) return fwd2_dispatch<32>((hipStream_t)stream, a, var);
@@ -626,6 +652,7 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     if (a.Nk <= kB3Keys) return dp == 32 ? bwd3_run<32, 8, 1, true>(st, a) : bwd3_run<64, 8, 1, true>(st, a);
     return dp == 32 ? bwd2_run_default<32, true>(st, a) : bwd2_run_default<64, true>(st, a);
   }
+  if (var != 1 && vec && cls_ok(d)) return cls_run<true>((hipStream_t)stream, a);
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;

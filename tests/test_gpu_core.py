@@ -27,7 +27,10 @@ CASES = [
     (1, 130, 70, 2, 96, "bf16"),                 # head dim 96 in 128-wide tiles, Nq != Nk
     (3, 16, 16, 4, 10, "f32"),                   # TNT inner attention, D = 10 (scalar path)
     (3, 16, 16, 4, 6, "bf16"),                   # TNT-B inner, D = 6
-    (2, 1, 197, 8, 48, "bf16"),                  # CaiT class attention (Nq = 1)
+    (2, 1, 197, 8, 48, "bf16"),                  # CaiT class attention (Nq = 1: K/V stream kernels)
+    (2, 1, 197, 4, 128, "bf16"),                 # Nq = 1 at head dim 128 (two chunks per lane)
+    (1, 1, 1000, 2, 40, "bf16"),                 # Nq = 1, many key passes, head dim not a chunk multiple of 64
+    (3, 1, 12, 3, 64, "bf16"),                   # CeiT LCA in bf16
     (2, 1, 12, 3, 64, "f32"),                    # CeiT LCA (Nq = 1, Nk = 12)
     (2, 100, 37, 3, 32, "bf16"),                 # CvT-style Nq != Nk
     (1, 1, 1, 1, 64, "f32"),                     # single key
