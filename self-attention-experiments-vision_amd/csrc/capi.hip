@@ -1264,7 +1264,7 @@ static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
 
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
   if (M < 1 || C < 1) return 0;
-  return ((size_t)ln_bwd_blocks(M) + kLnSplit) * 3 * C * sizeof(float);   // room for the scaled form
+  return (size_t)ln_bwd_blocks(M) * 3 * C * sizeof(float);   // room for the scaled form
 }
 
 static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
@@ -1341,21 +1341,10 @@ static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
   }
 #undef LNB
   if (int rc = check_launch("layernorm_bwd")) return rc;
-  float* part2 = a.part + (size_t)a.nblk * np * C;
-  if (sc) {
-    hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
-                       (const float*)a.part, a.nblk, part2);
-    if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
-    hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
-                       kLnSplit, (float*)nullptr);
-  } else {
-    hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, dim3((C + 63) / 64, kLnSplit), dim3(256), 0, st, a,
-                       (const float*)a.part, a.nblk, part2);
-    if (int rc = check_launch("layernorm_bwd_reduce")) return rc;
-    hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, dim3((C + 63) / 64, 1), dim3(256), 0, st, a, (const float*)part2,
-                       kLnSplit, (float*)nullptr);
-  }
-  return check_launch("layernorm_bwd_reduce2");
+  const dim3 rg((np * (C / 4) + 15) / 16);
+  if (sc) hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, rg, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, rg, dim3(256), 0, st, a);
+  return check_launch("layernorm_bwd_reduce");
 }
 
 const char* sae_last_error(void) { return g_err.c_str(); }

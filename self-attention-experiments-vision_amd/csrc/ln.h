@@ -196,39 +196,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
   }
 }
 
-// dgamma / dbeta = sum of the workgroup partials in workgroup order (deterministic), two levels
-// so that no thread walks a long dependent chain of loads: blockIdx.y = p of kLnSplit sums
-// partials [p*nblk/kLnSplit, (p+1)*nblk/kLnSplit) into part2[p] (256 threads = 64 columns x 4
-// strided groups, group sums in order); the final pass (gridDim.y == 1, nblk == kLnSplit, reading
-// part2) writes dgamma / dbeta.
-constexpr int kLnSplit = 16;
+// dgamma / dbeta (/ dlsc) = sum of the workgroup partials, deterministic, in ONE launch: thread
+// (column chunk col, group g) sums partials g, g + 16, ... (float4 columns, L2-hot), then the 16
+// group sums are added in group order.  A workgroup covers 16 float4 columns of the NP outputs.
+constexpr int kLnRedGroups = 16;
 template <int NP = 2>
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a, const float* src, int nsrc, float* dst) {
-  __shared__ float red[4][NP][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int per = (nsrc + gridDim.y - 1) / gridDim.y;
-  const int b0 = blockIdx.y * per, b1 = min(nsrc, b0 + per);
-  float sum[NP];
-#pragma unroll
-  for (int j = 0; j < NP; ++j) sum[j] = 0.f;
-  if (c < a.C) {
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a) {
+  __shared__ f32x4 red[kLnRedGroups][16];
+  const int C4 = a.C >> 2;
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;           // [0, NP * C4)
+  const bool ok = col < NP * C4;
+  const int which = ok ? col / C4 : 0, c4 = ok ? col % C4 : 0;
+  f32x4 s0 = {}, s1 = {};
+  if (ok) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.part) + (size_t)which * C4 + c4;
+    const size_t step = (size_t)NP * C4;          // one workgroup partial
+    int b = grp;
 #pragma unroll 4
-    for (int b = b0 + grp; b < b1; b += 4) {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) sum[j] += src[((size_t)b * NP + j) * a.C + c];
+    for (; b + kLnRedGroups < a.nblk; b += 2 * kLnRedGroups) {
+      s0 += src[(size_t)b * step];
+      s1 += src[(size_t)(b + kLnRedGroups) * step];
     }
+    if (b < a.nblk) s0 += src[(size_t)b * step];
   }
-#pragma unroll
-  for (int j = 0; j < NP; ++j) red[grp][j][cl] = sum[j];
+  red[grp][cl] = s0 + s1;
   __syncthreads();
-  if (grp == 0 && c < a.C) {
+  if (grp == 0 && ok) {
+    f32x4 t = red[0][cl];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const float t = ((red[0][j][cl] + red[1][j][cl]) + red[2][j][cl]) + red[3][j][cl];
-      if (dst) dst[((size_t)blockIdx.y * NP + j) * a.C + c] = t;
-      else (j == 0 ? a.dgamma : j == 1 ? a.dbeta : a.dlsc)[c] = t;
-    }
+    for (int g = 1; g < kLnRedGroups; ++g) t += red[g][cl];
+    float* dst = which == 0 ? a.dgamma : which == 1 ? a.dbeta : a.dlsc;
+    reinterpret_cast<f32x4*>(dst)[c4] = t;
   }
 }
 
