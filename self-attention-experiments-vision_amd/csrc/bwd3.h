@@ -367,10 +367,11 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
           const bf16x8 pf = acc_frag<__bf16>(sp[j], s2);
           const bf16x8 sf = acc_frag<__bf16>(dp[j], s2);
           // dS^T (bf16) for the dQ product: registers 8 s2 .. + 7 = query rows 16 s2 + 4h + {0..3, 8..11}
-          typedef __attribute__((ext_vector_type(4))) short s16x4_;
-          const s16x8 sv = __builtin_bit_cast(s16x8, sf);
-          *reinterpret_cast<s16x4_*>(img + wa[j][2 * s2]) = s16x4_{sv[0], sv[1], sv[2], sv[3]};
-          *reinterpret_cast<s16x4_*>(img + wa[j][2 * s2 + 1]) = s16x4_{sv[4], sv[5], sv[6], sv[7]};
+          // (whole dwords of the packed fragment: element-wise bf16 extraction made the compiler
+          // convert every dS value a second time and re-pack the pairs with v_perm)
+          const uint4 su = __builtin_bit_cast(uint4, sf);
+          *reinterpret_cast<uint2*>(img + wa[j][2 * s2]) = make_uint2(su.x, su.y);
+          *reinterpret_cast<uint2*>(img + wa[j][2 * s2 + 1]) = make_uint2(su.z, su.w);
 #pragma unroll
           for (int tt = 0; tt < NT; ++tt) {
             adv[j][tt] = MF<__bf16>::mma(gt[tt], pf, adv[j][tt]);

@@ -463,6 +463,58 @@ def rotary(x: torch.Tensor, base: float = 10000.0) -> torch.Tensor:
     return _Rotary.apply(x, float(base))
 
 
+# ------------------------------------------------------------------ gradient sinks (flat DP buffer)
+# The multi-rank step keeps every parameter gradient in one flat fp32 buffer (train.py).  Left to
+# autograd, each parameter gradient would be computed into a fresh tensor and then ADDED into its
+# zeroed flat view (one extra elementwise kernel per parameter, ~150 per DeiT-S step).  A sink is
+# that flat view: the backward kernels of this module (weight / bias GEMMs, LayerNorm dgamma /
+# dbeta, patch embedding) write the gradient straight into it and hand autograd None for that
+# parameter.  A parameter may feed at most one such op per backward (each Dense / LayerNorm of the
+# models is applied once per step); a second write raises instead of silently overwriting.
+_GRAD_SINKS = {}      # id(param) -> (weakref(param), fp32 view shaped like the param)
+_SINK_WRITTEN = set()
+
+
+def set_grad_sinks(params, views=None) -> None:
+    """Register ``views[i]`` (fp32, contiguous, shaped like ``params[i]``) as the gradient sink of
+    ``params[i]``; ``params=None`` clears every sink."""
+    import weakref
+    if params is None:
+        _GRAD_SINKS.clear()
+        return
+    for p, v in zip(params, views):
+        if v.dtype != torch.float32 or not v.is_contiguous() or v.shape != p.shape:
+            raise ValueError("set_grad_sinks: a sink must be an fp32 contiguous view shaped like its parameter")
+        _GRAD_SINKS[id(p)] = (weakref.ref(p), v)
+
+
+def begin_backward_sinks() -> None:
+    """Start of a step's backward: every sink may be written once again."""
+    _SINK_WRITTEN.clear()
+
+
+def _sink(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The sink of parameter ``t`` (or of the parameter ``t`` is a full reshape view of), viewed as
+    ``t``'s shape; None when it has none."""
+    if t is None or not t.requires_grad or not _GRAD_SINKS:
+        return None
+    base = t if t._base is None else t._base
+    e = _GRAD_SINKS.get(id(base))
+    if e is None or e[0]() is not base or t.numel() != base.numel():
+        return None
+    return e[1].view(t.shape)
+
+
+def _claim(sink: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Mark a sink as written by this backward (at most once per step)."""
+    if sink is not None:
+        key = sink.data_ptr()
+        if key in _SINK_WRITTEN:
+            raise RuntimeError("gradient sink written twice in one backward: a parameter feeds two ops")
+        _SINK_WRITTEN.add(key)
+    return sink
+
+
 # ------------------------------------------------------------------------------ projections
 def gemm_dw(x2: torch.Tensor, dy2: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor] = None,
             accumulate: bool = False, jblock: int = 0) -> None:
@@ -570,6 +622,7 @@ class _Dense(torch.autograd.Function):
         ctx.save_for_backward(x2, wd)
         ctx.has_b, ctx.xshape, ctx.xdtype = b is not None, x.shape, x.dtype
         ctx.wmeta = [(w.shape[1], w.dtype) for w in ws]
+        ctx.sinks_w, ctx.sink_b = [_sink(w) for w in ws], _sink(b)
         return y.view(*x.shape[:-1], J)
 
     @staticmethod
@@ -585,14 +638,30 @@ class _Dense(torch.autograd.Function):
             dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
         widths = [n for n, _ in ctx.wmeta]
         blocked = len(widths) > 1 and len(set(widths)) == 1 and widths[0] % 4 == 0
+        sw, sb = ctx.sinks_w, ctx.sink_b
         if _dw_ok(x2, dy2) and (blocked or len(widths) == 1):
-            db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
+            # flat-buffer sinks (multi-rank step): dW / db written in place, autograd gets None
+            db = _claim(sb) if sb is not None else (
+                torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None)
+            rdb = None if sb is not None else db
             if blocked:   # one contiguous [I, n] gradient per column block: no slice copies
-                dwb = torch.empty((len(widths), I, widths[0]), dtype=torch.float32, device=x2.device)
-                gemm_dw(x2, dy2, dwb, db, jblock=widths[0])
-                return (dx, db, None, *[dwb[k].to(wdt) for k, (_, wdt) in enumerate(ctx.wmeta)])
+                n = widths[0]
+                s0 = sw[0]
+                if s0 is not None and all(t is not None and t.data_ptr() == s0.data_ptr() + k * I * n * 4
+                                          for k, t in enumerate(sw)):   # adjacent sinks: one [nb, I, n] block
+                    for t in sw:
+                        _claim(t)
+                    gemm_dw(x2, dy2, s0.as_strided((len(widths), I, n), (I * n, n, 1)), db, jblock=n)
+                    return (dx, rdb, None, *[None] * len(widths))
+                dwb = torch.empty((len(widths), I, n), dtype=torch.float32, device=x2.device)
+                gemm_dw(x2, dy2, dwb, db, jblock=n)
+                return (dx, rdb, None, *[dwb[k].to(wdt) for k, (_, wdt) in enumerate(ctx.wmeta)])
+            if sw[0] is not None:
+                gemm_dw(x2, dy2, _claim(sw[0]), db)
+                return dx, rdb, None, None
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             gemm_dw(x2, dy2, dw, db)
+            db = rdb
         elif _dw_ok(x2, dy2):
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             db = torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None
@@ -648,6 +717,7 @@ class _PatchEmbed(torch.autograd.Function):
             _TIMER.end(tok, (desc.batch * Lp, w.shape[0], E))
         ctx.save_for_backward(images)
         ctx.desc, ctx.wshape, ctx.wdtype, ctx.has_b = desc, tuple(w.shape), w.dtype, b is not None
+        ctx.sinks = (_sink(w), _sink(b))
         return out
 
     @staticmethod
@@ -656,13 +726,15 @@ class _PatchEmbed(torch.autograd.Function):
         (images,) = ctx.saved_tensors
         desc = ctx.desc
         dout = dout.to(torch.bfloat16).contiguous()
-        dw = torch.empty(ctx.wshape, dtype=torch.float32, device=dout.device)
-        db = torch.empty((ctx.wshape[1],), dtype=torch.float32, device=dout.device) if ctx.has_b else None
+        sw, sb = ctx.sinks   # flat-buffer sinks (multi-rank step): written in place
+        dw = _claim(sw) if sw is not None else torch.empty(ctx.wshape, dtype=torch.float32, device=dout.device)
+        db = _claim(sb) if sb is not None else (
+            torch.empty((ctx.wshape[1],), dtype=torch.float32, device=dout.device) if ctx.has_b else None)
         ws = torch.empty(lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8,
                          device=dout.device)
         L.check(lib.sae_patch_embed_bwd(_stream(dout), ctypes.byref(desc), _ptr(images), _ptr(dout), _ptr(dw),
                                         _ptr(db), 0, _ptr(ws)))
-        return None, dw.to(ctx.wdtype), db, None, None
+        return None, None if sw is not None else dw.to(ctx.wdtype), _unsunk(db, sb), None, None
 
 
 def patch_embed(images: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], patch: Tuple[int, int],
@@ -777,6 +849,7 @@ class _FFBlock(torch.autograd.Function):
         y = gemm_nt(a, w1t, b1)   # K = hidden (1536): 42 vs 44 us for the library GEMM
         ctx.save_for_backward(x2, h, a, w0p, w1p)
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
+        ctx.sinks = [_sink(t) for t in (w0, b0, w1, b1)]
         return y.view(*x.shape[:-1], w1.shape[1])
 
     @staticmethod
@@ -788,14 +861,19 @@ class _FFBlock(torch.autograd.Function):
         if dy2.stride(1) != 1 or dy2.stride(0) % 8 or dy2.data_ptr() % 16:
             dy2 = dy2.contiguous()
         dh = gemm_nt(dy2, w1p, None, EPI_DGELU, aux=h)            # dA W1^T, times gelu'(h)
-        dw1 = torch.empty((Hd, O), dtype=torch.float32, device=dy2.device)
-        db1 = torch.empty((O,), dtype=torch.float32, device=dy2.device) if ctx.has_b[1] else None
+        sw0, sb0, sw1, sb1 = ctx.sinks   # flat-buffer sinks (multi-rank step): written in place
+        dev = dy2.device
+        dw1 = _claim(sw1) if sw1 is not None else torch.empty((Hd, O), dtype=torch.float32, device=dev)
+        db1 = _claim(sb1) if sb1 is not None else (
+            torch.empty((O,), dtype=torch.float32, device=dev) if ctx.has_b[1] else None)
         gemm_dw(a, dy2, dw1, db1)
         dx = gemm_nt(dh, w0p) if use_gemm_nt(Hd) else dh @ w0p.t()   # dH W0^T
-        dw0 = torch.empty((I, Hd), dtype=torch.float32, device=dy2.device)
-        db0 = torch.empty((Hd,), dtype=torch.float32, device=dy2.device) if ctx.has_b[0] else None
+        dw0 = _claim(sw0) if sw0 is not None else torch.empty((I, Hd), dtype=torch.float32, device=dev)
+        db0 = _claim(sb0) if sb0 is not None else (
+            torch.empty((Hd,), dtype=torch.float32, device=dev) if ctx.has_b[0] else None)
         gemm_dw(x2, dh, dw0, db0)
-        return dx.view(ctx.xshape).to(ctx.xdtype), dw0, db0, dw1, db1
+        ret = [None if sk is not None else g for sk, g in zip(ctx.sinks, (dw0, db0, dw1, db1))]
+        return (dx.view(ctx.xshape).to(ctx.xdtype), *ret)
 
 
 FF_FUSED = True   # tools/ab_step.py flips this to A/B against the library GEMM + torch GELU path
@@ -857,7 +935,7 @@ def _ln_fwd(x, delta, gamma, beta, eps):
     return xout, y, mean, rstd
 
 
-def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta):
+def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta, sinks=(None, None)):
     lib = L.load()
     C = xs.shape[-1]
     M = xs.numel() // C
@@ -865,8 +943,8 @@ def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta):
     dy = _bf16c(dy)
     dx = torch.empty_like(xs)
     ddelta = torch.empty(xs.shape, dtype=torch.bfloat16, device=xs.device) if want_ddelta else None
-    dg = torch.empty(C, dtype=torch.float32, device=xs.device)
-    db = torch.empty(C, dtype=torch.float32, device=xs.device)
+    dg = _claim(sinks[0]) if sinks[0] is not None else torch.empty(C, dtype=torch.float32, device=xs.device)
+    db = _claim(sinks[1]) if sinks[1] is not None else torch.empty(C, dtype=torch.float32, device=xs.device)
     ws = torch.empty(lib.sae_layernorm_bwd_workspace_bytes(M, C), dtype=torch.uint8, device=xs.device)
     if dxin is not None:
         dxin = _f32c(dxin, "dxin")
@@ -875,18 +953,24 @@ def _ln_bwd(xs, mean, rstd, gamma, dy, dxin, want_ddelta):
     return dx, ddelta, dg, db
 
 
+def _unsunk(g, sink):
+    """The gradient autograd should see: None when it went into a sink."""
+    return None if sink is not None else g
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps):
         _, y, mean, rstd = _ln_fwd(x, None, gamma, beta, eps)
         ctx.save_for_backward(x, mean, rstd, gamma)
+        ctx.sinks = (_sink(gamma), _sink(beta))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, rstd, gamma = ctx.saved_tensors
-        dx, _, dg, db = _ln_bwd(x, mean, rstd, gamma, dy, None, False)
-        return dx, dg, db, None
+        dx, _, dg, db = _ln_bwd(x, mean, rstd, gamma, dy, None, False, ctx.sinks)
+        return dx, _unsunk(dg, ctx.sinks[0]), _unsunk(db, ctx.sinks[1]), None
 
 
 class _AddLayerNorm(torch.autograd.Function):
@@ -895,6 +979,7 @@ class _AddLayerNorm(torch.autograd.Function):
         xout, y, mean, rstd = _ln_fwd(x, delta, gamma, beta, eps)
         ctx.save_for_backward(xout, mean, rstd, gamma)
         ctx.delta_dtype = delta.dtype
+        ctx.sinks = (_sink(gamma), _sink(beta))
         return xout, y
 
     @staticmethod
@@ -902,8 +987,8 @@ class _AddLayerNorm(torch.autograd.Function):
         xout, mean, rstd, gamma = ctx.saved_tensors
         if dy is None:
             dy = torch.zeros(xout.shape, dtype=torch.bfloat16, device=xout.device)
-        dx, ddelta, dg, db = _ln_bwd(xout, mean, rstd, gamma, dy, dxout, True)
-        return dx, ddelta.to(ctx.delta_dtype), dg, db, None
+        dx, ddelta, dg, db = _ln_bwd(xout, mean, rstd, gamma, dy, dxout, True, ctx.sinks)
+        return dx, ddelta.to(ctx.delta_dtype), _unsunk(dg, ctx.sinks[0]), _unsunk(db, ctx.sinks[1]), None
 
 
 class _AddLayerNormScaled(torch.autograd.Function):
@@ -928,6 +1013,7 @@ class _AddLayerNormScaled(torch.autograd.Function):
                                              _ptr(rowscale), int(rpb)))
         ctx.save_for_backward(xout, mean, rstd, gamma, delta, lsf, rowscale)
         ctx.rpb, ctx.delta_dtype, ctx.ls_dtype = int(rpb), delta_dtype, ls.dtype
+        ctx.sinks = (_sink(gamma), _sink(beta), _sink(ls) if ls.dtype == torch.float32 else None)
         return xout, y
 
     @staticmethod
@@ -943,14 +1029,16 @@ class _AddLayerNormScaled(torch.autograd.Function):
         dxin = _f32c(dxout, "dxin") if dxout is not None else None
         dx = torch.empty_like(xout)
         ddelta = torch.empty(xout.shape, dtype=torch.bfloat16, device=xout.device)
-        dg = torch.empty(C, dtype=torch.float32, device=xout.device)
-        db = torch.empty(C, dtype=torch.float32, device=xout.device)
-        dls = torch.empty(C, dtype=torch.float32, device=xout.device)
+        sg, sbt, sls = ctx.sinks
+        dg = _claim(sg) if sg is not None else torch.empty(C, dtype=torch.float32, device=xout.device)
+        db = _claim(sbt) if sbt is not None else torch.empty(C, dtype=torch.float32, device=xout.device)
+        dls = _claim(sls) if sls is not None else torch.empty(C, dtype=torch.float32, device=xout.device)
         ws = torch.empty(lib.sae_layernorm_bwd_workspace_bytes(M, C), dtype=torch.uint8, device=xout.device)
         L.check(lib.sae_layernorm_bwd_scaled(_stream(xout), M, C, _ptr(xout), _ptr(mean), _ptr(rstd), _ptr(gamma),
                                              _ptr(dy), _ptr(dxin), _ptr(dx), _ptr(ddelta), _ptr(dg), _ptr(db),
                                              _ptr(ws), _ptr(delta), _ptr(lsf), _ptr(rowscale), ctx.rpb, _ptr(dls)))
-        return dx, ddelta.to(ctx.delta_dtype), dg, db, dls.to(ctx.ls_dtype), None, None, None
+        return (dx, ddelta.to(ctx.delta_dtype), _unsunk(dg, sg), _unsunk(db, sbt),
+                None if sls is not None else dls.to(ctx.ls_dtype), None, None, None)
 
 
 def add_layer_norm_scaled(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,

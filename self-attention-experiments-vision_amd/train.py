@@ -60,7 +60,8 @@ class TrainStep:
 
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
                  label_smoothing: float = 0.1, bucket_cap_mb: float = 64.0, device: Optional[torch.device] = None,
-                 graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None):
+                 graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None,
+                 grad_sinks: bool = True):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
@@ -95,6 +96,12 @@ class TrainStep:
                     hi = lo
             if hi > 0:
                 self._buckets.append((0, hi))
+            # the backward kernels write each parameter's gradient straight into its flat view
+            # (ops.set_grad_sinks) instead of autograd adding a fresh gradient tensor into it
+            self._sinks = bool(grad_sinks)
+            if self._sinks:
+                from . import ops
+                ops.set_grad_sinks(params, [p.grad for p in params])
         base_lr = lr * (global_batch / 512)
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         if self.graph:
@@ -136,6 +143,9 @@ class TrainStep:
 
     def _fwd_bwd(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         self._zero_grad()
+        if self.flat and self._sinks:
+            from . import ops
+            ops.begin_backward_sinks()
         if self.input_layout == "NHWC":
             logits = self.model(images, is_training=True)
         else:

@@ -35,3 +35,36 @@ def test_graph_step_matches_eager(dev, flat):
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         err = float((pe - pg).abs().max())
         assert err <= 1e-3 * max(1.0, float(pe.abs().max())), (n, err)
+
+
+@pytest.mark.parametrize("model", ["deit_ti_patch16", "cait"])
+def test_flat_grad_sinks_bitwise(dev, model):
+    """The multi-rank step's in-place gradient sinks (ops.set_grad_sinks: the backward kernels write
+    every Dense / FF / LayerNorm / patch-embedding gradient straight into its view of the flat
+    buffer) give the same gradient bits as autograd's own accumulation, and a parameter
+    feeding two sink-writing ops in one backward is refused."""
+    from sae_vision_amd import cait, ops, train, vit
+    torch.manual_seed(0)
+    if model == "cait":
+        m_a = cait.create_cait("cait_xxs_24", 1000, torch.bfloat16, stoch_depth=False, device=dev)
+    else:
+        m_a = vit.create_model(model, 1000, torch.bfloat16, device=dev)
+    m_b = copy.deepcopy(m_a)
+    m_b.load_state_dict(m_a.state_dict())
+    s_a = train.TrainStep(m_a, global_batch=8, device=dev, flat_grads=False)
+    s_b = train.TrainStep(m_b, global_batch=8, device=dev, flat_grads=True)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(8, 224, 224, 3, device=dev, generator=g)
+    y = torch.randint(0, 1000, (8,), device=dev, generator=g)
+    s_a._fwd_bwd(x, y)
+    s_b._fwd_bwd(x, y)
+    torch.cuda.synchronize()
+    for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
+        assert pa.grad is not None and pb.grad is not None, n
+        assert pb.grad.data_ptr() >= s_b._flat.data_ptr(), n            # still the flat view
+        assert torch.equal(pa.grad, pb.grad), (n, float((pa.grad - pb.grad).abs().max()))
+    # a second backward without begin_backward_sinks() re-claims the sinks: refused
+    with pytest.raises(RuntimeError, match="written twice"):
+        logits = m_b(x, is_training=True)
+        train.smoothed_cross_entropy(logits, y).backward()
+    ops.set_grad_sinks(None)
