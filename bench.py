@@ -237,9 +237,12 @@ def main():
     ap.add_argument("--no-headline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="training loop only (for rocprofv3 runs)")
     ap.add_argument("--eager", action="store_true", help="N=1: eager step instead of the HIP-graph replay")
-    ap.add_argument("--flat-grads", action="store_true",
-                    help="N=1: the multi-rank step structure (flat gradient buffer, forward+backward graph and "
-                         "AdamW graph) without the collective, to rehearse the N > 1 step's GPU time")
+    ap.add_argument("--two-graphs", action="store_true",
+                    help="N=1: the multi-rank step structure (forward+backward graph, the all-reduce point, AdamW "
+                         "graph) without the collective, to rehearse the N > 1 step's GPU time")
+    ap.add_argument("--no-flat-grads", action="store_true",
+                    help="autograd's per-parameter gradients and torch's fused AdamW (the round-1 step) instead of "
+                         "the flat gradient buffer, in-place gradient sinks and the one-launch AdamW")
     ap.add_argument("--input-layout", default="HWCN", choices=["HWCN", "NHWC"],
                     help="HWCN: the reference's train-step feed [H, W, C, N] fp32 (train.py:80-81, "
                          "input_pipeline.py:187-191), gathered by the fused patch GEMM; NHWC: the model call")
@@ -269,7 +272,8 @@ def main():
     # forward + backward graph, bucketed RCCL all-reduce of the flat gradient, AdamW graph
     use_graph = not args.eager
     step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph, input_layout=args.input_layout,
-                           flat_grads=True if args.flat_grads else None, grad_sinks=not args.no_grad_sinks)
+                           flat_grads=False if args.no_flat_grads else None, grad_sinks=not args.no_grad_sinks,
+                           two_graphs=True if args.two_graphs else None)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
     if args.input_layout == "HWCN":
@@ -346,7 +350,7 @@ def main():
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
-                   "step": ("hip_graph_replay" if world == 1 and not args.flat_grads else "hip_graphs+rccl_allreduce") if use_graph
+                   "step": ("hip_graph_replay" if not step.two_graphs else "hip_graphs+rccl_allreduce") if use_graph
                    else "eager"},
         "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,

@@ -275,6 +275,31 @@ int sae_layernorm_bwd_scaled(void* stream, int32_t M, int32_t C, const float* x,
                              const void* delta, const float* layerscale, const float* rowscale,
                              int32_t rows_per_sample, float* dlayerscale);
 
+/* Optimizer update of the data-parallel training step (train.py:25-27,229-233: optax.adamw,
+   survey D9 descent), every parameter in ONE launch.  The parameters are cut into chunks of
+   SAE_ADAMW_CHUNK elements; sae_adamw_plan (host only, no GPU call) fills that chunk table for
+   n_items fp32 tensors (item i: parameter p[i], gradient g[i], moments m[i], v[i], n[i] elements,
+   contiguous) into `chunks` (capacity max_chunks) and returns the count in *n_chunks.  The caller
+   copies the table to device memory once; sae_adamw_step then increments the device-resident
+   step counter *step (int32) and applies, with t = the new *step (torch.optim.AdamW order):
+     p *= 1 - lr*wd;  m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2;
+     p -= lr/(1 - b1^t) * m / (sqrt(v)/sqrt(1 - b2^t) + eps)
+   Both launches are stream-ordered, so a captured graph replays with the right t. */
+#define SAE_ADAMW_CHUNK 2048
+typedef struct sae_adamw_chunk {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int32_t n;     /* elements of this chunk, <= SAE_ADAMW_CHUNK */
+  int32_t vec;   /* set by the plan: 16-byte aligned full chunk (vector path) */
+} sae_adamw_chunk;
+int sae_adamw_plan(int32_t n_items, float* const* p, const float* const* g, float* const* m,
+                   float* const* v, const int64_t* n, sae_adamw_chunk* chunks, int64_t max_chunks,
+                   int64_t* n_chunks);
+int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int32_t* step,
+                   float lr, float beta1, float beta2, float eps, float weight_decay);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);
 

@@ -81,6 +81,8 @@ _PROTOS = [
     ("sae_layernorm_fwd_scaled", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp,
                                         _i32]),
     ("sae_layernorm_bwd_scaled", _i32, [_vp, _i32, _i32] + [_vp] * 14 + [_i32, _vp]),
+    ("sae_adamw_plan", _i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    ("sae_adamw_step", _i32, [_vp, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32]),
     ("sae_last_error", ctypes.c_char_p, []),
     ("sae_abi_version", _i32, []),
     ("sae_build_info", ctypes.c_char_p, []),
@@ -95,6 +97,15 @@ class WeightCastItem(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("w16", ctypes.c_void_p), ("wt16", ctypes.c_void_p),
                 ("K", ctypes.c_int32), ("N", ctypes.c_int32), ("ld16", ctypes.c_int32), ("ldT", ctypes.c_int32),
                 ("col0", ctypes.c_int32)]
+
+
+class AdamwChunk(ctypes.Structure):
+    """Mirror of ``sae_adamw_chunk`` (include/sae_attn.h)."""
+    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("n", ctypes.c_int32), ("vec", ctypes.c_int32)]
+
+
+SAE_ADAMW_CHUNK = 2048
 
 
 class SaeError(RuntimeError):

@@ -24,6 +24,7 @@
 #include "gemm_nt.h"
 #include "patch.h"
 #include "ln.h"
+#include "adamw.h"
 
 using namespace sae;
 
@@ -1292,6 +1293,49 @@ int sae_layernorm_bwd_scaled(void* stream, int32_t M, int32_t C, const float* x,
     return fail(SAE_EINVAL, "layernorm_bwd_scaled: layerscale needs 16-byte, delta 8-byte alignment");
   return ln_bwd_impl(stream, M, C, x, mean, rstd, gamma, dy, dxin, dx, ddelta, dgamma, dbeta, workspace, delta,
                      layerscale, rowscale, rows_per_sample, dlayerscale);
+}
+
+// ---------------------------------------------------------------------------------- AdamW
+static_assert(sizeof(sae_adamw_chunk) == sizeof(AdamwChunk) && SAE_ADAMW_CHUNK == kAdamwChunk,
+              "sae_adamw_chunk mirrors AdamwChunk");
+
+int sae_adamw_plan(int32_t n_items, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* n, sae_adamw_chunk* chunks, int64_t max_chunks, int64_t* n_chunks) {
+  if (n_items < 0 || !n_chunks || (n_items > 0 && (!p || !g || !m || !v || !n)))
+    return fail(SAE_EINVAL, "adamw_plan: bad arguments");
+  int64_t k = 0;
+  for (int32_t i = 0; i < n_items; ++i) {
+    if (n[i] < 0 || (n[i] > 0 && (!p[i] || !g[i] || !m[i] || !v[i])))
+      return fail(SAE_EINVAL, "adamw_plan: item %d invalid", i);
+    for (int64_t off = 0; off < n[i]; off += SAE_ADAMW_CHUNK, ++k) {
+      if (k < max_chunks && chunks) {
+        sae_adamw_chunk& c = chunks[k];
+        c.p = p[i] + off;
+        c.g = g[i] + off;
+        c.m = m[i] + off;
+        c.v = v[i] + off;
+        c.n = (int32_t)std::min<int64_t>(SAE_ADAMW_CHUNK, n[i] - off);
+        c.vec = c.n == SAE_ADAMW_CHUNK && aligned16(c.p) && aligned16(c.g) && aligned16(c.m) && aligned16(c.v);
+      }
+    }
+  }
+  *n_chunks = k;
+  if (k > max_chunks) return fail(SAE_EINVAL, "adamw_plan: %lld chunks > capacity %lld", (long long)k,
+                                  (long long)max_chunks);
+  return ok();
+}
+
+int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int32_t* step, float lr,
+                   float beta1, float beta2, float eps, float weight_decay) {
+  if (n_chunks < 0 || n_chunks >= (1LL << 31) || (n_chunks > 0 && !chunks) || !step)
+    return fail(SAE_EINVAL, "adamw_step: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adamw_tick_kernel, dim3(1), dim3(64), 0, st, step);
+  if (int rc = check_launch("adamw_tick")) return rc;
+  if (n_chunks == 0) return ok();
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st,
+                     reinterpret_cast<const AdamwChunk*>(chunks), step, lr, beta1, beta2, eps, weight_decay);
+  return check_launch("adamw");
 }
 
 static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,

@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
-__all__ = ["smoothed_cross_entropy", "TrainStep", "init_distributed"]
+__all__ = ["smoothed_cross_entropy", "TrainStep", "init_distributed", "FusedAdamW"]
 
 
 def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.1) -> torch.Tensor:
@@ -51,6 +51,55 @@ def init_distributed():
     return rank, world, local
 
 
+class FusedAdamW:
+    """AdamW (optax.adamw of train.py:25-27,229-233, torch.optim.AdamW's update order) for fp32 GPU
+    parameters whose gradients live in one flat buffer: every parameter in one HIP launch
+    (``sae_adamw_step``, csrc/adamw.h) instead of torch's multi-tensor launches.  The moments are
+    two more flat buffers laid out like the gradients; the step counter stays on the device, so the
+    update can be captured in a HIP graph and replayed."""
+
+    def __init__(self, params, flat_grad: torch.Tensor, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        import ctypes
+        from . import _lib as L
+        self.lib = L.load()
+        self.params = list(params)
+        self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
+        dev = flat_grad.device
+        self.m = torch.zeros_like(flat_grad)
+        self.v = torch.zeros_like(flat_grad)
+        self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        n = len(self.params)
+        P = (ctypes.c_void_p * n)()
+        G, M, V = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+        N = (ctypes.c_int64 * n)()
+        for i, p in enumerate(self.params):
+            g = p.grad
+            if (p.dtype != torch.float32 or not p.is_contiguous() or g is None or g.dtype != torch.float32
+                    or not g.is_contiguous() or g.data_ptr() < flat_grad.data_ptr()):
+                raise ValueError("FusedAdamW: fp32 contiguous parameters with views of the flat gradient buffer")
+            off = (g.data_ptr() - flat_grad.data_ptr()) // 4
+            P[i], G[i] = p.data_ptr(), g.data_ptr()
+            M[i], V[i] = self.m.data_ptr() + 4 * off, self.v.data_ptr() + 4 * off
+            N[i] = p.numel()
+        cap = sum((p.numel() + L.SAE_ADAMW_CHUNK - 1) // L.SAE_ADAMW_CHUNK for p in self.params)
+        table = (L.AdamwChunk * max(1, cap))()
+        cnt = ctypes.c_int64(0)
+        L.check(self.lib.sae_adamw_plan(n, P, G, M, V, N, table, cap, ctypes.byref(cnt)))
+        self.n_chunks = int(cnt.value)
+        self.table = torch.frombuffer(bytearray(table), dtype=torch.uint8).to(dev)   # device copy, built once
+
+    def step(self):
+        from . import _lib as L
+        b1, b2 = self.betas
+        st = torch.cuda.current_stream(self.m.device).cuda_stream
+        L.check(self.lib.sae_adamw_step(st, self.n_chunks, self.table.data_ptr(), self.step_count.data_ptr(),
+                                        self.lr, b1, b2, self.eps, self.weight_decay))
+
+    def state_tensors(self):
+        return [self.m, self.v, self.step_count]
+
+
 class TrainStep:
     """``step(images, labels)`` = forward (bf16 compute) + loss + backward (+ bucketed RCCL
     all-reduce of the flat gradient when world > 1) + optimizer update.  No host sync.
@@ -61,7 +110,7 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
                  label_smoothing: float = 0.1, bucket_cap_mb: float = 64.0, device: Optional[torch.device] = None,
                  graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None,
-                 grad_sinks: bool = True):
+                 grad_sinks: bool = True, two_graphs: Optional[bool] = None):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
@@ -73,9 +122,13 @@ class TrainStep:
         self._params = params
         if self.world > 1:
             self._broadcast_from_rank0([t for t in model.state_dict().values() if torch.is_tensor(t)])
-        # flat_grads (default: world > 1) selects the multi-rank step structure: flat gradient
-        # buffer + two graphs around the all-reduce (settable at world 1 to test that structure)
-        self.flat = self.world > 1 if flat_grads is None else bool(flat_grads)
+        # flat_grads (default: on the GPU, and whenever world > 1): one flat gradient buffer written
+        # in place by the backward kernels (gradient sinks), stepped by the one-launch FusedAdamW;
+        # two_graphs (default: world > 1): forward + backward and the optimizer as two graphs
+        # around the all-reduce (settable at world 1 to test that structure)
+        on_gpu = all(p.is_cuda for p in params)
+        self.flat = (self.world > 1 or on_gpu) if flat_grads is None else bool(flat_grads)
+        self.two_graphs = self.world > 1 if two_graphs is None else bool(two_graphs)
         if self.flat:
             # one flat fp32 gradient buffer, every .grad a view into it (autograd accumulates into
             # the views in place), cut into buckets of ~bucket_cap_mb along parameter boundaries
@@ -104,12 +157,16 @@ class TrainStep:
                 ops.set_grad_sinks(params, [p.grad for p in params])
         base_lr = lr * (global_batch / 512)
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
-        if self.graph:
-            kw["capturable"] = True   # step counters on the device: replayable
-        try:
-            self.opt = torch.optim.AdamW(params, fused=True, **kw)
-        except (RuntimeError, TypeError):
-            self.opt = torch.optim.AdamW(params, foreach=True, **kw)
+        self.opt = None
+        if self.flat and on_gpu and all(p.dtype == torch.float32 and p.is_contiguous() for p in params):
+            self.opt = FusedAdamW(params, self._flat, **kw)
+        else:
+            if self.graph:
+                kw["capturable"] = True   # step counters on the device: replayable
+            try:
+                self.opt = torch.optim.AdamW(params, fused=True, **kw)
+            except (RuntimeError, TypeError):
+                self.opt = torch.optim.AdamW(params, foreach=True, **kw)
         self.smoothing = label_smoothing
 
     @staticmethod
@@ -183,7 +240,9 @@ class TrainStep:
         self._labels = labels.clone()
         params = self._params
         snap = [p.detach().clone() for p in params]
-        had_state = {id(p) for p in params if p in self.opt.state and self.opt.state[p]}
+        fused = isinstance(self.opt, FusedAdamW)
+        snap_fused = [t.clone() for t in self.opt.state_tensors()] if fused else None
+        had_state = set() if fused else {id(p) for p in params if p in self.opt.state and self.opt.state[p]}
         snap_state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                       for p in params if id(p) in had_state}
         s = torch.cuda.Stream(device=images.device)
@@ -198,7 +257,10 @@ class TrainStep:
         with torch.no_grad():
             for p, v in zip(params, snap):
                 p.copy_(v)
-            for p in params:
+            if fused:
+                for t, v in zip(self.opt.state_tensors(), snap_fused):
+                    t.copy_(v)
+            for p in ([] if fused else params):
                 st = self.opt.state.get(p)
                 if not st:
                     continue
@@ -213,7 +275,7 @@ class TrainStep:
         if not self.flat:
             self.opt.zero_grad(set_to_none=True)
         try:
-            if not self.flat:     # the whole step in one graph
+            if not self.two_graphs:     # the whole step in one graph
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._loss = self._eager(self._images, self._labels)

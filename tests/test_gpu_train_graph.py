@@ -9,16 +9,19 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("flat", [False, True])
-def test_graph_step_matches_eager(dev, flat):
-    """flat=True: the multi-rank structure (flat gradient buffer, forward + backward graph, the
-    all-reduce point, optimizer graph) at world 1, against the plain eager step."""
+@pytest.mark.parametrize("split", [False, True])
+def test_graph_step_matches_eager(dev, split):
+    """The graph step (flat gradient buffer with in-place sinks, one-launch FusedAdamW) against the
+    round-1 eager step (autograd's per-parameter gradients, torch's AdamW); split=True: the
+    multi-rank structure (forward + backward graph, the all-reduce point, optimizer graph) at
+    world 1."""
     from sae_vision_amd import train, vit
     torch.manual_seed(0)
     m_e = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
     m_g = copy.deepcopy(m_e)
-    s_e = train.TrainStep(m_e, global_batch=8, device=dev)
-    s_g = train.TrainStep(m_g, global_batch=8, device=dev, graph=True, flat_grads=flat)
+    s_e = train.TrainStep(m_e, global_batch=8, device=dev, flat_grads=False)
+    s_g = train.TrainStep(m_g, global_batch=8, device=dev, graph=True, two_graphs=split)
+    assert s_g.flat and isinstance(s_g.opt, train.FusedAdamW) and not s_e.flat
     g = torch.Generator(device=dev).manual_seed(3)
     data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
              torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(4)]
@@ -26,7 +29,7 @@ def test_graph_step_matches_eager(dev, flat):
     # (executing nothing) and replays once: exactly one optimizer step on data[0], as eager
     le = [float(s_e(*data[0]))]
     lg = [float(s_g(*data[0]))]
-    assert s_g._g is not None and (s_g._g_opt is not None) == flat
+    assert s_g._g is not None and (s_g._g_opt is not None) == split
     for x, y in data[1:]:
         le.append(float(s_e(x, y)))
         lg.append(float(s_g(x, y)))
@@ -68,3 +71,35 @@ def test_flat_grad_sinks_bitwise(dev, model):
         logits = m_b(x, is_training=True)
         train.smoothed_cross_entropy(logits, y).backward()
     ops.set_grad_sinks(None)
+
+
+def test_fused_adamw_matches_torch(dev):
+    """sae_adamw_step (one launch over every parameter, chunk table built once, device step
+    counter) against torch.optim.AdamW on the same gradients for several steps: odd sizes (scalar
+    tail chunks) and sizes past one chunk."""
+    from sae_vision_amd import train
+    g = torch.Generator(device=dev).manual_seed(11)
+    shapes = [(384, 1152), (7,), (1000,), (3, 2051), (384,)]
+    ref = [torch.randn(s, device=dev, generator=g) for s in shapes]
+    mine = [t.clone() for t in ref]
+    for t in ref + mine:
+        t.requires_grad_(True)
+    flat = torch.zeros(sum(t.numel() for t in mine), device=dev)
+    off = 0
+    for t in mine:
+        t.grad = flat[off:off + t.numel()].view_as(t)
+        off += t.numel()
+    kw = dict(lr=3e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
+    opt_ref = torch.optim.AdamW(ref, foreach=False, **kw)
+    opt = train.FusedAdamW(mine, flat, **kw)
+    for _ in range(5):
+        for a, b in zip(ref, mine):
+            gr = torch.randn(a.shape, device=dev, generator=g)
+            a.grad = gr.clone()
+            b.grad.copy_(gr)
+        opt_ref.step()
+        opt.step()
+    assert int(opt.step_count.item()) == 5
+    for a, b in zip(ref, mine):
+        err = float((a.detach() - b.detach()).abs().max() / a.detach().abs().max())
+        assert err <= 2e-6, err
