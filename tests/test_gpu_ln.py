@@ -14,7 +14,7 @@ from _util import rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M,C", [(25216, 384), (1000, 768), (37, 192), (5, 1024), (3, 4)])
+@pytest.mark.parametrize("M,C", [(25216, 384), (1000, 768), (37, 192), (5, 1024), (3, 4), (37, 384), (11, 512), (3, 128)])
 @pytest.mark.parametrize("with_delta", [False, True])
 def test_add_layer_norm(dev, M, C, with_delta):
     import torch
