@@ -846,7 +846,10 @@ class _FFBlock(torch.autograd.Function):
         w0p, w0t = _cast([w0], torch.bfloat16)
         w1p, w1t = _cast([w1], torch.bfloat16)
         a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
-        y = gemm_nt(a, w1t, b1)   # K = hidden (1536): 42 vs 44 us for the library GEMM
+        # Dense_1 forward is a plain GEMM + bias: sae_gemm_nt up to K = hidden 1536 (DeiT-S: 42 vs 44 us for
+        # the library), the library beyond (ViT-B hidden 3072: 82 vs 100 us, profiles/r01_gemm_probe_v13.txt)
+        y = gemm_nt(a, w1t, b1) if Hd <= FF_NT_MAX_HIDDEN else torch.addmm(b1.to(a.dtype), a, w1p) if b1 is not None \
+            else a @ w1p
         ctx.save_for_backward(x2, h, a, w0p, w1p)
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
         ctx.sinks = [_sink(t) for t in (w0, b0, w1, b1)]
@@ -877,6 +880,7 @@ class _FFBlock(torch.autograd.Function):
 
 
 FF_FUSED = True   # tools/ab_step.py flips this to A/B against the library GEMM + torch GELU path
+FF_NT_MAX_HIDDEN = 2048   # Dense_1 forward on sae_gemm_nt up to this reduction depth (hidden width)
 
 
 def ff_block_ok(x: torch.Tensor, w0: torch.Tensor, w1: torch.Tensor) -> bool:
