@@ -949,7 +949,7 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
     hipLaunchKernelGGL(gemm_dw_kernel<false>, dim3((unsigned)grid), dim3(256), lds, st, a);
   if (int rc = check_launch("gemm_dw")) return rc;
   const long long n4 = (long long)I * J / 4;
-  const unsigned rb = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+  const unsigned rb = (unsigned)std::min<long long>((n4 + kDwRedCols - 1) / kDwRedCols, 4096);
   hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3(rb, db ? 2 : 1), dim3(256), 0, st, a);
   return check_launch("gemm_dw_reduce");
 }
@@ -1147,7 +1147,7 @@ int sae_patch_embed_bwd(void* stream, const sae_patch_desc* d, const void* image
                 : (f32 ? patch_dw_launch<false, true>(st, a, grid) : patch_dw_launch<false, false>(st, a, grid));
   if (rc) return rc;
   const long long n4 = (long long)K * J / 4;
-  const unsigned rb = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+  const unsigned rb = (unsigned)std::min<long long>((n4 + kDwRedCols - 1) / kDwRedCols, 4096);
   hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3(rb, db ? 2 : 1), dim3(256), 0, st, a);
   if (int rc2 = check_launch("patch_embed_dw_reduce")) return rc2;
   return ok();
@@ -1385,7 +1385,7 @@ static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
   }
 #undef LNB
   if (int rc = check_launch("layernorm_bwd")) return rc;
-  const dim3 rg((np * (C / 4) + 15) / 16);
+  const dim3 rg((np * (C / 4) + kLnRedCols - 1) / kLnRedCols);
   if (sc) hipLaunchKernelGGL(ln_bwd_reduce_kernel<3>, rg, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ln_bwd_reduce_kernel<2>, rg, dim3(256), 0, st, a);
   return check_launch("layernorm_bwd_reduce");

@@ -216,14 +216,35 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   }
 }
 
-// dw[i][j] (+)= sum_s part[s][i][j] in split order; db likewise (blockIdx.y == 1 for db)
+// dw[i][j] (+)= sum_s part[s][i][j]; db likewise (blockIdx.y == 1 for db).  A workgroup takes 64
+// float4 columns x 4 split groups: group g sums its contiguous quarter of the splits in split order,
+// then the four group sums are added in group order (fixed order: deterministic).  One thread per
+// column summing all S partials (S = 14 .. 56 at the DeiT-S shapes) ran latency-bound on a few
+// hundred workgroups.
+constexpr int kDwRedCols = 64, kDwRedGroups = 4;
 __global__ __launch_bounds__(256) void gemm_dw_reduce_kernel(DwArgs a) {
   if (blockIdx.y == 0) {
+    __shared__ f32x4 red[kDwRedGroups][kDwRedCols];
     const long long n4 = (long long)a.I * a.J / 4;
     const long long stride = (long long)a.I * a.J;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n4; e += (long long)gridDim.x * 256) {
-      f32x4 acc = *reinterpret_cast<const f32x4*>(a.part + 4 * e);
-      for (int s = 1; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(a.part + s * stride + 4 * e);
+    const int col = threadIdx.x % kDwRedCols, grp = threadIdx.x / kDwRedCols;
+    const int per = (a.S + kDwRedGroups - 1) / kDwRedGroups;
+    const int s0 = grp * per, s1 = min(a.S, s0 + per);
+    for (long long base = blockIdx.x * (long long)kDwRedCols; base < n4; base += (long long)gridDim.x * kDwRedCols) {
+      const long long e = base + col;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (e < n4 && s0 < s1) {
+        acc = *reinterpret_cast<const f32x4*>(a.part + s0 * stride + 4 * e);
+        for (int s = s0 + 1; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(a.part + s * stride + 4 * e);
+      }
+      red[grp][col] = acc;
+      __syncthreads();
+      if (grp == 0 && e < n4) {
+#pragma unroll
+        for (int g = 1; g < kDwRedGroups; ++g) acc += red[g][col];
+      }
+      __syncthreads();
+      if (grp != 0 || e >= n4) continue;
       const long long i = (4 * e) / a.J, j = (4 * e) % a.J;
       f32x4* out = reinterpret_cast<f32x4*>(
           a.jblock ? a.dw + (j / a.jblock) * ((long long)a.I * a.jblock) + i * a.jblock + j % a.jblock

@@ -197,15 +197,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
 }
 
 // dgamma / dbeta (/ dlsc) = sum of the workgroup partials, deterministic, in ONE launch: thread
-// (column chunk col, group g) sums partials g, g + 16, ... (float4 columns, L2-hot), then the 16
-// group sums are added in group order.  A workgroup covers 16 float4 columns of the NP outputs.
-constexpr int kLnRedGroups = 16;
+// (column chunk col, group g) sums partials g, g + 64, ... (float4 columns, L2-hot), then the 64
+// group sums are added in group order.  A workgroup covers 4 float4 columns of the NP outputs
+// (16 groups x 16 columns left each thread 64 dependent-latency partials on a dozen workgroups).
+constexpr int kLnRedGroups = 64;
+constexpr int kLnRedCols = 256 / kLnRedGroups;
 template <int NP = 2>
 __global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(LnArgs a) {
-  __shared__ f32x4 red[kLnRedGroups][16];
+  __shared__ f32x4 red[kLnRedGroups][kLnRedCols];
   const int C4 = a.C >> 2;
-  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int col = blockIdx.x * 16 + cl;           // [0, NP * C4)
+  const int cl = threadIdx.x % kLnRedCols, grp = threadIdx.x / kLnRedCols;
+  const int col = blockIdx.x * kLnRedCols + cl;   // [0, NP * C4)
   const bool ok = col < NP * C4;
   const int which = ok ? col / C4 : 0, c4 = ok ? col % C4 : 0;
   f32x4 s0 = {}, s1 = {};
