@@ -502,6 +502,9 @@ def _sink(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     e = _GRAD_SINKS.get(id(base))
     if e is None or e[0]() is not base or t.numel() != base.numel():
         return None
+    g = base.grad   # a sink is live only while it is still the parameter's .grad (not replaced / reset)
+    if g is None or g.data_ptr() != e[1].data_ptr():
+        return None
     return e[1].view(t.shape)
 
 

@@ -103,3 +103,26 @@ def test_fused_adamw_matches_torch(dev):
     for a, b in zip(ref, mine):
         err = float((a.detach() - b.detach()).abs().max() / a.detach().abs().max())
         assert err <= 2e-6, err
+
+
+def test_grad_sink_follows_param_grad(dev):
+    """A sink is only used while it is still the parameter's .grad: after the gradient is reset
+    (zero_grad(set_to_none=True)) autograd's own accumulation takes over again."""
+    from sae_vision_amd import ops, vit
+    torch.manual_seed(0)
+    m = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
+    params = [p for p in m.parameters()]
+    flat = torch.zeros(sum(p.numel() for p in params), device=dev)
+    off = 0
+    for p in params:
+        p.grad = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    ops.set_grad_sinks(params, [p.grad for p in params])
+    for p in params:
+        p.grad = None            # reset: the registered views are no longer the gradients
+    ops.begin_backward_sinks()
+    x = torch.randn(2, 224, 224, 3, device=dev)
+    m(x, is_training=True).float().sum().backward()
+    assert all(p.grad is not None for p in params)
+    assert float(flat.abs().max()) == 0.0   # nothing went into the stale views
+    ops.set_grad_sinks(None)
