@@ -617,7 +617,7 @@ class _Dense(torch.autograd.Function):
         J = sum(w.shape[1] for w in ws)
         x2 = x.to(dt).reshape(-1, I)
         wd, wt = _cast(ws, dt)
-        if wt is not None and use_gemm_nt(I) and _nt_ok(x2, J):
+        if wt is not None and use_gemm_nt(I, J) and _nt_ok(x2, J):
             y = gemm_nt(x2, wt, b)                        # bias in the epilogue
         else:
             # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
@@ -635,7 +635,7 @@ class _Dense(torch.autograd.Function):
         dy2 = dy.reshape(-1, J)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
             dy2 = dy2.contiguous()
-        if use_gemm_nt(J) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
+        if use_gemm_nt(J, I) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
         else:
             dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
@@ -774,14 +774,20 @@ EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 
 
 # sae_gemm_nt vs the library GEMM at the training shapes (tools/gemm_probe.py,
-# profiles/r01_gemm_probe_v11.txt): the HIP kernel wins for reduction depths <= 384 (DeiT-S QKV
-# forward 37 vs 78 us, output projection 17 vs 21 us), the library for the deeper ones
-# (K = 768 .. 1536); the FF block always fuses its GELU / GELU' into sae_gemm_nt.
+# profiles/r01_gemm_probe_v11.txt, profiles/r02_gemm_probe_pin_ab.txt): the HIP kernel wins for
+# reduction depths <= 384 (DeiT-S QKV forward 35 vs 78 us, output projection 16 vs 24 us) and
+# ties or wins on the narrow (384-feature) input gradients up to K = 1536 (DeiT-S / CaiT QKV dX
+# 33.7 vs 35.6 us, FF Dense_0 dX 43.1 vs 43.0); the library keeps the deep, wide ViT-B shapes
+# (K 768 .. 3072 into 768 .. 3072 features: 780 vs 840-1090 TF/s); the FF block always fuses its
+# GELU / GELU' into sae_gemm_nt.
 GEMM_NT_MAX_K = 512
+GEMM_NT_NARROW_N = 384
+GEMM_NT_NARROW_MAX_K = 1536
 
 
-def use_gemm_nt(K: int) -> bool:
-    return K <= GEMM_NT_MAX_K
+def use_gemm_nt(K: int, N: int) -> bool:
+    """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt."""
+    return K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
 
 
 def _nt_ok(a2: torch.Tensor, N: int) -> bool:
@@ -873,7 +879,7 @@ class _FFBlock(torch.autograd.Function):
         db1 = _claim(sb1) if sb1 is not None else (
             torch.empty((O,), dtype=torch.float32, device=dev) if ctx.has_b[1] else None)
         gemm_dw(a, dy2, dw1, db1)
-        dx = gemm_nt(dh, w0p) if use_gemm_nt(Hd) else dh @ w0p.t()   # dH W0^T
+        dx = gemm_nt(dh, w0p) if use_gemm_nt(Hd, I) else dh @ w0p.t()   # dH W0^T
         dw0 = _claim(sw0) if sw0 is not None else torch.empty((I, Hd), dtype=torch.float32, device=dev)
         db0 = _claim(sb0) if sb0 is not None else (
             torch.empty((Hd,), dtype=torch.float32, device=dev) if ctx.has_b[0] else None)
