@@ -13,9 +13,11 @@
 // which removes the two elementwise HBM passes (GELU forward, GELU backward) per FF block.
 //
 // Structure (gfx950): a 128 x 128 output tile per 256-thread workgroup, 4 waves of 64 x 64 (2 x 2
-// v_mfma_f32_32x32x16_bf16 accumulators); 64-deep K stages staged global -> registers -> LDS
-// ([128 rows][64 k] images, 128-byte rows XOR-swizzled per row: conflict-free ds_read_b128), two
-// LDS buffers, loads issued two stages ahead.  The MFMA runs with the output feature as the
+// v_mfma_f32_32x32x16_bf16 accumulators); BK-deep K stages staged global -> registers -> LDS
+// ([128 rows][BK k] images, rows XOR-swizzled per row: conflict-free ds_read_b128), two LDS
+// buffers, loads issued two stages ahead.  BK = 64 (64 KiB of LDS, 2 workgroups per CU) by
+// default; BK = 32 (32 KiB, 3-4 workgroups per CU) for the GELU / GELU' epilogues at K <= 384,
+// where more resident tiles let one tile's epilogue VALU run under other tiles' MFMAs.  The MFMA runs with the output feature as the
 // accumulator row and the token on the lane, so the epilogue writes each token's features as
 // packed bf16x4 into a per-wave LDS image and stores whole 128-byte row segments.
 // XCD-aware order: the N tiles of one token block are consecutive on one XCD (the token rows are
@@ -87,50 +89,59 @@ __device__ __forceinline__ unsigned dgelu_bf2(unsigned dw, unsigned hw) {   // d
   return f2_to_bf2(bf2_to_f2(dw) * ((x * q) * poly + s));
 }
 
-// one operand's 128 x 64 stage: 1024 16-byte chunks, 4 per thread
-struct NtStage {
-  uint4 v[4];
-  unsigned goff[4];
-  unsigned loff[4];
+// one operand's 128 x BK stage: 16 * BK 16-byte chunks, BK / 16 per thread
+template <int BK> struct NtStageT {
+  static constexpr int CPR = BK / 8;         // 16-byte chunks per row
+  static constexpr int PER = 128 * CPR / 256;
+  uint4 v[PER];
+  unsigned goff[PER];
+  unsigned loff[PER];
   __device__ __forceinline__ void init(int tid, long long ld) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < PER; ++i) {
       const int id = tid + 256 * i;
-      const int r = id >> 3, c = id & 7;
+      const int r = id / CPR, c = id % CPR;
       goff[i] = (unsigned)(((long long)r * ld + 8 * c) * 2);
-      loff[i] = r * 128 + 16 * (c ^ swz<64>(r));
+      loff[i] = r * (BK * 2) + 16 * (c ^ swz<BK>(r));
     }
   }
   __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned koff) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < PER; ++i)
       v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i] + koff, 0, 0));
   }
   __device__ __forceinline__ void write(char* img) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
+    for (int i = 0; i < PER; ++i) *reinterpret_cast<uint4*>(img + loff[i]) = v[i];
   }
 };
+using NtStage = NtStageT<kNtK>;
 
 // A-operand loader of the plain GEMM: rows m0 .. m0 + 127 of the row-major a [M][K] through a
-// buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders; a loader
-// also maps GEMM row m to its output row (orow).
-struct NtRowA {
-  NtStage s;
+// buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders (64-deep
+// stages); a loader also maps GEMM row m to its output row (orow).
+template <int BK> struct NtRowAT {
+  static constexpr int kBK = BK;
+  NtStageT<BK> s;
   __amdgpu_buffer_rsrc_t rs;
   __device__ __forceinline__ void init(const NtArgs& a, int tid, int m0) {
     rs = row_rsrc(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
     s.init(tid, a.lda);
   }
-  __device__ __forceinline__ void load(const NtArgs&, int st) { s.load(rs, (unsigned)st * (kNtK * 2)); }
+  __device__ __forceinline__ void load(const NtArgs&, int st) { s.load(rs, (unsigned)st * (BK * 2)); }
   __device__ __forceinline__ void write(char* img) const { s.write(img); }
   static __device__ __forceinline__ long long orow(const NtArgs&, int m) { return m; }
 };
+using NtRowA = NtRowAT<kNtK>;
+
+template <class AL> struct NtDepth { static constexpr int value = kNtK; };
+template <int BK> struct NtDepth<NtRowAT<BK>> { static constexpr int value = BK; };
 
 template <int EPI, class AL = NtRowA>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
+__global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ? 3 : 4) : 2) void gemm_nt_kernel(NtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int IMG = kNtT * kNtK * 2;   // 16 KiB per operand image
+  constexpr int BK = NtDepth<AL>::value;   // K per stage
+  constexpr int IMG = kNtT * BK * 2;       // one operand image (16 KiB at BK = 64)
   const int tn = (a.N + kNtT - 1) / kNtT;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / tn, nt = bid % tn;
@@ -142,13 +153,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   // rows past N read zero through the descriptor's range check
   const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
   AL as[2];
-  NtStage bs[2];
+  NtStageT<BK> bs[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     as[q].init(a, tid, m0);
     bs[q].init(tid, a.ldb);
   }
-  const int nst = a.K / kNtK;
+  const int nst = a.K / BK;
   // Straight-line staging (no data-dependent branches around the loads and LDS writes): the
   // loads of stages st + 2 and the LDS writes of stage st + 1 are issued unconditionally --
   // past the end they read zeros (descriptor range check) or unused bytes into a buffer nobody
@@ -157,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
   as[0].load(a, 0);
   bs[0].load(rb, 0);
   as[1].load(a, 1);
-  bs[1].load(rb, kNtK * 2);
+  bs[1].load(rb, BK * 2);
   // kEpiDGelu: this lane's eight aux chunks (the epilogue's row groups) are loaded before the
   // main loop, so their HBM traffic overlaps the MFMAs instead of following them
   const int c8 = lane & 7;                 // 16-byte chunk of an epilogue row segment
@@ -181,11 +192,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
 
   auto compute = [&](const char* ima, const char* imb) {
 #pragma unroll
-    for (int s = 0; s < kNtK / 16; ++s) {
-      const bf16x8 b0 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + r, s, h);
-      const bf16x8 b1 = Img<__bf16, 64>::rowfrag(imb, 64 * wn + 32 + r, s, h);
-      const bf16x8 a0 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + r, s, h);
-      const bf16x8 a1 = Img<__bf16, 64>::rowfrag(ima, 64 * wm + 32 + r, s, h);
+    for (int s = 0; s < BK / 16; ++s) {
+      const bf16x8 b0 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + r, s, h);
+      const bf16x8 b1 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + 32 + r, s, h);
+      const bf16x8 a0 = Img<__bf16, BK>::rowfrag(ima, 64 * wm + r, s, h);
+      const bf16x8 a1 = Img<__bf16, BK>::rowfrag(ima, 64 * wm + 32 + r, s, h);
       acc[0][0] = MF<__bf16>::mma(b0, a0, acc[0][0]);
       acc[0][1] = MF<__bf16>::mma(b0, a1, acc[0][1]);
       acc[1][0] = MF<__bf16>::mma(b1, a0, acc[1][0]);
@@ -203,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NtArgs a) {
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
       // register set bsel went to LDS at the end of the previous stage: refill it (stage + 2)
       as[bsel].load(a, st + bsel + 2);
-      bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (kNtK * 2));
+      bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (BK * 2));
       compute(ima, ima + IMG);
       as[bsel ^ 1].write(nxt);
       bs[bsel ^ 1].write(nxt + IMG);
