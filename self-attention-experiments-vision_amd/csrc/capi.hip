@@ -478,6 +478,18 @@ int th_bwd(void* stream, const sae_attn_desc* d, const void* q, const void* k, c
 }
 
 // ==================================================================================== C ABI
+// one gemm_dw launch (with or without the bias column sums), NG wave groups per workgroup
+template <class XL, class YL, int NG>
+static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hipStream_t st) {
+  const void* fn = bias ? (const void*)gemm_dw_kernel<true, XL, YL, NG> : (const void*)gemm_dw_kernel<false, XL, YL, NG>;
+  if (int rc = lds_attr(fn, lds)) return rc;
+  if (bias)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, XL, YL, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+  else
+    hipLaunchKernelGGL((gemm_dw_kernel<false, XL, YL, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+  return 0;
+}
+
 // one sae_gemm_nt launch: 128 x 128 tiles, two LDS stage buffers of BK-deep A and B images
 template <int EPI, class AL>
 static int nt_launch(const NtArgs& g, long long grid, hipStream_t st) {
@@ -880,12 +892,13 @@ int sae_th_attn_bwd_rotary(void* stream, const sae_attn_desc* d, const void* q, 
 }
 
 // ------------------------------------------------------------------ projection gradients
-static void dw_plan(int M, int I, int J, int* S, int* chunk) {
-  // at most 512 workgroups = one resident round (2 per CU x 256 CUs): a 513th would run alone in
-  // a second round (the old ceil() rule launched 513 / 540 / 513 for the DeiT-S QKV / FF / output
-  // projections)
+static void dw_plan(int M, int I, int J, int* S, int* chunk, int slots = 512) {
+  // at most `slots` workgroups = one resident round (512: 2 per CU x 256 CUs; 256 for the 8-wave
+  // two-group kernel): a 513th would run alone in a second round (the old ceil() rule launched
+  // 513 / 540 / 513 for the DeiT-S QKV / FF / output projections).  A smaller slot count gives
+  // fewer splits, so the 512-slot plan's workspace bounds every plan's.
   const int tiles = ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
-  int s = 512 / tiles;
+  int s = slots / tiles;
   s = std::max(1, std::min(s, (M + 255) / 256));
   int c = (M + s - 1) / s;
   c = (c + kDwK - 1) / kDwK * kDwK;
@@ -934,8 +947,14 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
   a.M = M;
   a.I = I;
   a.J = J;
-  dw_plan(M, I, J, &a.S, &a.chunk);
-  if ((long long)a.chunk * std::max(ldx, ldy) * 2 >= (1LL << 31))
+  // wave groups per workgroup (gemm_dw.h): two for small outputs (<= 64 tiles of 128 x 128: every
+  // DeiT-S / CaiT projection), where half the splits still fill the chip and halve the fp32
+  // partial traffic (output projection dW + reduce 34.8 -> 30.6 us); one for the larger ViT-B
+  // outputs, where halving the splits would leave CUs idle (FF 139 -> 205 us)
+  const int tiles = ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
+  const int NG = tiles <= 64 ? 2 : 1;
+  dw_plan(M, I, J, &a.S, &a.chunk, 512 / NG);
+  if ((long long)(a.chunk + 4 * NG * kDwK) * std::max(ldx, ldy) * 2 >= (1LL << 31))
     return fail(SAE_EUNSUPPORTED, "gemm_dw: token chunk exceeds 32-bit buffer addressing");
   a.part = reinterpret_cast<float*>(workspace);
   a.bpart = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) +
@@ -949,13 +968,14 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
   a.jblock = jblock;
   hipStream_t st = (hipStream_t)stream;
   const long long grid = (long long)a.S * ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
-  const size_t lds = 4 * kDwK * 256;
-  if (int rc = lds_attr((const void*)gemm_dw_kernel<true>, lds)) return rc;
-  if (int rc = lds_attr((const void*)gemm_dw_kernel<false>, lds)) return rc;
-  if (db)
-    hipLaunchKernelGGL(gemm_dw_kernel<true>, dim3((unsigned)grid), dim3(256), lds, st, a);
-  else
-    hipLaunchKernelGGL(gemm_dw_kernel<false>, dim3((unsigned)grid), dim3(256), lds, st, a);
+  const size_t lds = NG * 4 * kDwK * 256;
+  typedef DwRow<false> XR;
+  typedef DwRow<true> YR;
+  if (NG == 2) {
+    if (int rc = dw_launch<XR, YR, 2>(a, db != nullptr, grid, lds, st)) return rc;
+  } else {
+    if (int rc = dw_launch<XR, YR, 1>(a, db != nullptr, grid, lds, st)) return rc;
+  }
   if (int rc = check_launch("gemm_dw")) return rc;
   const long long n4 = (long long)I * J / 4;
   const unsigned rb = (unsigned)std::min<long long>((n4 + kDwRedCols - 1) / kDwRedCols, 4096);

@@ -94,9 +94,13 @@ __device__ __forceinline__ bf16x8 dw_colfrag(const char* img, const unsigned* ca
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <bool BIAS, class XL = DwRow<false>, class YL = DwRow<true>>
-__global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// NG = 2: two groups of 4 waves per workgroup split the token chunk's stages (group g takes
+// stages g, g + 2, ...; own LDS buffers) and add their accumulators through LDS at the end, group
+// 0 first (fixed order): half the splits, so half the fp32 partial-tile traffic, at the same number
+// of waves in flight (one 8-wave workgroup per CU instead of two 4-wave ones).
+template <bool BIAS, class XL = DwRow<false>, class YL = DwRow<true>, int NG = 1>
+__global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void gemm_dw_kernel(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_all[];
   constexpr int IMG = kDwK * 256;     // 16 KiB per operand image
   const int ti = (a.I + kDwT - 1) / kDwT, tj = (a.J + kDwT - 1) / kDwT;
   // XCD-aware order: the logical blocks of one XCD are a contiguous range, tiles fastest, so
@@ -106,7 +110,9 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
   const int tile = bid % (ti * tj), s = bid / (ti * tj);
   const int it = tile % ti, jt = tile / ti;
   const int i0 = it * kDwT, j0 = jt * kDwT;
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int tid = threadIdx.x & 255, lane = tid & 63, h = lane >> 5;
+  const int grp = NG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+  char* const smem = smem_all + grp * 4 * IMG;   // this group's two stage buffers
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = w & 1, wj = w >> 1;  // this wave's 64 x 64 quarter
   const int m0 = s * a.chunk;
@@ -122,14 +128,16 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
     xs[r].init(a, tid, m0, m1, i0);
     ys[r].init(a, tid, m0, m1, j0);
   }
-  const int nst = (m1 - m0 + kDwK - 1) / kDwK;
+  // this group's stage count (group g's stage q is the chunk's stage NG q + g; past the chunk's
+  // end the rows read zero)
+  const int nst = ((m1 - m0 + kDwK - 1) / kDwK + NG - 1) / NG;
   // straight-line staging (as gemm_nt.h): stage loads / LDS writes past the end are issued
   // unconditionally (they read zeros: rows past m1 are zero) so the waitcnt pass keeps two
   // register stages in flight instead of draining the queue before every reload
-  xs[0].load(a, 0);
-  ys[0].load(a, 0);
-  xs[1].load(a, 1);
-  ys[1].load(a, 1);
+  xs[0].load(a, grp);
+  ys[0].load(a, grp);
+  xs[1].load(a, NG + grp);
+  ys[1].load(a, NG + grp);
 
   unsigned ca[8];   // [operand x / dy][t = 0, 1][r1, r2] transposed-read addresses
   {
@@ -183,8 +191,8 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
       const char* imx = smem + bsel * 2 * IMG;
       char* nxt = smem + (bsel ^ 1) * 2 * IMG;
       // register set bsel was written to LDS at the end of the previous stage: refill (stage + 2)
-      xs[bsel].load(a, st + bsel + 2);
-      ys[bsel].load(a, st + bsel + 2);
+      xs[bsel].load(a, (st + bsel + 2) * NG + grp);
+      ys[bsel].load(a, (st + bsel + 2) * NG + grp);
       compute(imx, imx + IMG);
       xs[bsel ^ 1].write(nxt);
       ys[bsel ^ 1].write(nxt + IMG);
@@ -192,6 +200,37 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_kernel(DwArgs a) {
     }
   }
   if (st < nst) compute(smem, smem + IMG);   // odd stage count: the last stage sits in buffer 0
+  if constexpr (NG == 2) {
+    // group 1 hands its accumulators to group 0 through the (now free) stage buffers: per wave
+    // 16 KiB of dW (+ 8 KiB of db), lane-contiguous
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem_all) + w * (4 * 16 * 64);
+    float* redb = reinterpret_cast<float*>(smem_all + 4 * 16384) + w * (2 * 16 * 64);
+    if (grp == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(q * 16 + r) * 64 + lane] = acc[q >> 1][q & 1][r];
+      if (bias) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) redb[(q * 16 + r) * 64 + lane] = accb[q][r];
+      }
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[q >> 1][q & 1][r] += red[(q * 16 + r) * 64 + lane];
+    if (bias) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accb[q][r] += redb[(q * 16 + r) * 64 + lane];
+    }
+  }
   // fp32 partial tile: accumulator row = i (row_of), column = j (lane)
   float* P = a.part + (size_t)s * a.I * a.J;
   const int jc = j0 + 64 * wj + (lane & 31);
