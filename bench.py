@@ -366,8 +366,9 @@ def main():
                    "model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": N,
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
-                   "step": ("hip_graph_replay" if not step.two_graphs else "hip_graphs+rccl_allreduce") if use_graph
-                   else "eager"},
+                   # what actually ran: a capture that failed leaves the step eager (train.py)
+                   "step": ("hip_graph_replay" if not step.two_graphs else "hip_graphs+rccl_allreduce")
+                   if use_graph and step.graph else "eager"},
         "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,
         "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,
