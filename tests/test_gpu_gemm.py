@@ -12,6 +12,8 @@ SHAPES = [  # (M, I, J)
     (25216, 384, 1152),   # DeiT-S QKV projection, batch 128
     (25216, 1536, 384),   # DeiT-S FF Dense_1
     (197, 768, 1000),     # ragged tokens, head-like J
+    (3000, 768, 1000),    # two wave groups, an odd stage count per group (10 stages per chunk)
+    (4616, 768, 2304),    # ViT-B QKV-like output (108 tiles > 64): one wave group per workgroup
     (1000, 24, 40),       # tiny, I/J below one tile
     (64, 8, 8),
 ]
