@@ -367,8 +367,9 @@ def main():
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
                    # what actually ran: a capture that failed leaves the step eager (train.py)
-                   "step": ("hip_graph_replay" if not step.two_graphs else "hip_graphs+rccl_allreduce")
-                   if use_graph and step.graph else "eager"},
+                   "step": ("hip_graph_replay" if not step.two_graphs else
+                            "hip_graphs+" + ("rccl" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend())
+                            + "_allreduce") if use_graph and step.graph else "eager"},
         "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,
         "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,
