@@ -300,6 +300,22 @@ int sae_adamw_plan(int32_t n_items, float* const* p, const float* const* g, floa
 int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int32_t* step,
                    float lr, float beta1, float beta2, float eps, float weight_decay);
 
+/* Label-smoothed softmax cross entropy of the training step (replaces train.py:77-90:
+   optax.smooth_labels(one_hot(labels), alpha) + jnp.mean(optax.softmax_cross_entropy)):
+     loss = mean_r [ lse_r - (1 - alpha) x[r, labels[r]] - (alpha / classes) sum_c x[r, c] ]
+   logits x [rows][classes] (row stride ld elements, dtype SAE_DTYPE_BF16 or SAE_DTYPE_F32),
+   labels int64 [rows] (a label outside [0, classes) contributes no target term).  fwd writes
+   lse [rows] (fp32, for the backward) and *loss (fp32, device memory); the row losses are summed
+   in row order (deterministic).  bwd writes dlogits [rows][classes] (row stride ldd, the logits'
+   dtype) = (*grad_loss / rows) (softmax(x_r) - (1 - alpha) onehot - alpha / classes).
+   rows <= SAE_CE_MAX_ROWS. */
+#define SAE_CE_MAX_ROWS 16384
+int sae_smoothed_ce_fwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
+                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* loss);
+int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
+                        int32_t dtype, const int64_t* labels, float alpha, const float* lse,
+                        const float* grad_loss, void* dlogits, int64_t ldd);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);
 

@@ -22,6 +22,7 @@
 #include "cls.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
+#include "loss.h"
 #include "patch.h"
 #include "ln.h"
 #include "adamw.h"
@@ -1298,6 +1299,53 @@ static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
   if (M < 1 || C < 1) return 0;
   return (size_t)ln_bwd_blocks(M) * 3 * C * sizeof(float);   // room for the scaled form
+}
+
+// ------------------------------------------------------------------ training loss
+static int ce_check(int32_t rows, int32_t classes, const void* logits, int64_t ld, int32_t dtype,
+                    const int64_t* labels) {
+  if (rows < 1 || rows > SAE_CE_MAX_ROWS || classes < 1 || ld < classes)
+    return fail(SAE_EINVAL, "smoothed_ce: rows %d (1..%d), classes %d, ld %lld", rows, SAE_CE_MAX_ROWS, classes,
+                (long long)ld);
+  if (dtype != SAE_DTYPE_BF16 && dtype != SAE_DTYPE_F32) return fail(SAE_EINVAL, "smoothed_ce: bad dtype %d", dtype);
+  if (!logits || !labels) return fail(SAE_EINVAL, "smoothed_ce: NULL logits / labels");
+  return 0;
+}
+
+int sae_smoothed_ce_fwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
+                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* loss) {
+  if (int rc = ce_check(rows, classes, logits, ld, dtype, labels)) return rc;
+  if (!lse || !loss) return fail(SAE_EINVAL, "smoothed_ce_fwd: NULL lse / loss");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)rows * 4;
+  if (dtype == SAE_DTYPE_BF16) {
+    if (int rc = lds_attr((const void*)smoothed_ce_fwd_kernel<__bf16>, lds)) return rc;
+    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<__bf16>, dim3(1), dim3(64 * kCeWaves), lds, st,
+                       reinterpret_cast<const __bf16*>(logits), (long long)ld, labels, rows, classes, alpha, lse, loss);
+  } else {
+    if (int rc = lds_attr((const void*)smoothed_ce_fwd_kernel<float>, lds)) return rc;
+    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<float>, dim3(1), dim3(64 * kCeWaves), lds, st,
+                       reinterpret_cast<const float*>(logits), (long long)ld, labels, rows, classes, alpha, lse, loss);
+  }
+  return check_launch("smoothed_ce_fwd");
+}
+
+int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
+                        int32_t dtype, const int64_t* labels, float alpha, const float* lse,
+                        const float* grad_loss, void* dlogits, int64_t ldd) {
+  if (int rc = ce_check(rows, classes, logits, ld, dtype, labels)) return rc;
+  if (!lse || !grad_loss || !dlogits || ldd < classes)
+    return fail(SAE_EINVAL, "smoothed_ce_bwd: NULL lse / grad_loss / dlogits or ldd < classes");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SAE_DTYPE_BF16)
+    hipLaunchKernelGGL(smoothed_ce_bwd_kernel<__bf16>, dim3(rows), dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(logits), (long long)ld, labels, rows, classes, alpha, lse,
+                       grad_loss, reinterpret_cast<__bf16*>(dlogits), (long long)ldd);
+  else
+    hipLaunchKernelGGL(smoothed_ce_bwd_kernel<float>, dim3(rows), dim3(256), 0, st,
+                       reinterpret_cast<const float*>(logits), (long long)ld, labels, rows, classes, alpha, lse,
+                       grad_loss, reinterpret_cast<float*>(dlogits), (long long)ldd);
+  return check_launch("smoothed_ce_bwd");
 }
 
 static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,

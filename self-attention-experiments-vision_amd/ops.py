@@ -1078,3 +1078,42 @@ def add_layer_norm(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, be
     returns ``(x + delta, LN(x + delta))``."""
     _require_gpu(x, delta)
     return _AddLayerNorm.apply(x, delta, gamma, beta, eps)
+
+
+# ------------------------------------------------------------------------------ training loss
+class _SmoothedCE(torch.autograd.Function):
+    """Label-smoothed softmax cross entropy, mean over rows (train.py:77-90: optax.smooth_labels +
+    jnp.mean(optax.softmax_cross_entropy)) in two HIP launches (sae_smoothed_ce_fwd / _bwd);
+    dlogits come back in the logits' dtype."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, alpha):
+        lib = L.load()
+        R, K = logits.shape
+        lse = torch.empty(R, dtype=torch.float32, device=logits.device)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        L.check(lib.sae_smoothed_ce_fwd(_stream(logits), R, K, _ptr(logits), logits.stride(0), dtype_code(logits.dtype),
+                                        _ptr(labels), float(alpha), _ptr(lse), _ptr(loss)))
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.alpha = float(alpha)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        lib = L.load()
+        logits, labels, lse = ctx.saved_tensors
+        R, K = logits.shape
+        g = gloss.float().contiguous()
+        dx = torch.empty((R, K), dtype=logits.dtype, device=logits.device)
+        L.check(lib.sae_smoothed_ce_bwd(_stream(logits), R, K, _ptr(logits), logits.stride(0), dtype_code(logits.dtype),
+                                        _ptr(labels), ctx.alpha, _ptr(lse), _ptr(g), _ptr(dx), dx.stride(0)))
+        return dx, None, None
+
+
+def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, alpha: float = 0.1) -> torch.Tensor:
+    """mean_r [lse_r - (1 - alpha) x[r, y_r] - (alpha / K) sum_c x[r, c]] of [R, K] GPU logits (bf16 or
+    fp32) against int64 labels [R]; the HIP kernels, or an error when they cannot take the input."""
+    _require_gpu(logits, labels)
+    if logits.dim() != 2 or logits.stride(1) != 1:
+        logits = logits.reshape(-1, logits.shape[-1]).contiguous()
+    return _SmoothedCE.apply(logits, labels.to(torch.int64).contiguous(), alpha)

@@ -29,6 +29,12 @@ __all__ = ["smoothed_cross_entropy", "TrainStep", "init_distributed", "FusedAdam
 
 
 def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.1) -> torch.Tensor:
+    """train.py:77-90 (optax.smooth_labels + mean softmax cross entropy): on the GPU the two-launch
+    HIP loss (ops.smoothed_cross_entropy); CPU tensors (the multi-process gloo tests' small
+    models) take torch's cross entropy, which computes the same quantity."""
+    if logits.is_cuda:
+        from . import ops
+        return ops.smoothed_cross_entropy(logits, labels, smoothing)
     return F.cross_entropy(logits.float(), labels, label_smoothing=smoothing)
 
 
