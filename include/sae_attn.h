@@ -300,6 +300,17 @@ int sae_adamw_plan(int32_t n_items, float* const* p, const float* const* g, floa
 int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int32_t* step,
                    float lr, float beta1, float beta2, float eps, float weight_decay);
 
+/* Encoder input of ViT / DeiT (models/vit.py:82-85 class-token concatenate, vit.py:46 +
+   position_embed.py:48 AddAbsPosEmbed), tokens bf16 [B][L][E] from the patch embedding, cls fp32
+   [E], pos fp32 [L+1][E]:  x fp32 [B][L+1][E] = concat(cls, float(tokens)) + pos.  Backward:
+   dtokens bf16 [B][L][E] = bf16(dx[:, 1:]), dpos [L+1][E] = sum_b dx[b], dcls [E] = dpos[0] (may be
+   NULL); batch sums in a fixed order.  E % 4 == 0, E <= 4096; x / dx / cls / pos / dpos / dcls
+   16-byte and tokens / dtokens 8-byte aligned. */
+int sae_tokens_fwd(void* stream, int32_t B, int32_t L, int32_t E, const void* tokens, const float* cls,
+                   const float* pos, float* x);
+int sae_tokens_bwd(void* stream, int32_t B, int32_t L, int32_t E, const float* dx, void* dtokens, float* dcls,
+                   float* dpos);
+
 /* Label-smoothed softmax cross entropy of the training step (replaces train.py:77-90:
    optax.smooth_labels(one_hot(labels), alpha) + jnp.mean(optax.softmax_cross_entropy)):
      loss = mean_r [ lse_r - (1 - alpha) x[r, labels[r]] - (alpha / classes) sum_c x[r, c] ]

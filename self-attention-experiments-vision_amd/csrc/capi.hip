@@ -23,6 +23,7 @@
 #include "gemm_dw.h"
 #include "gemm_nt.h"
 #include "loss.h"
+#include "tokens.h"
 #include "patch.h"
 #include "ln.h"
 #include "adamw.h"
@@ -1299,6 +1300,41 @@ static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
 size_t sae_layernorm_bwd_workspace_bytes(int32_t M, int32_t C) {
   if (M < 1 || C < 1) return 0;
   return (size_t)ln_bwd_blocks(M) * 3 * C * sizeof(float);   // room for the scaled form
+}
+
+// ------------------------------------------------------------------ encoder input tokens
+static int tokens_check(int32_t B, int32_t L, int32_t E) {
+  if (B < 1 || L < 1 || E < 4 || E % 4 || E > 4096)
+    return fail(SAE_EINVAL, "tokens: B %d, L %d, E %d (E a multiple of 4, <= 4096)", B, L, E);
+  return 0;
+}
+
+int sae_tokens_fwd(void* stream, int32_t B, int32_t L, int32_t E, const void* tokens, const float* cls,
+                   const float* pos, float* x) {
+  if (int rc = tokens_check(B, L, E)) return rc;
+  if (!tokens || !cls || !pos || !x) return fail(SAE_EINVAL, "tokens_fwd: NULL argument");
+  if (!aligned16(cls) || !aligned16(pos) || !aligned16(x) || ((uintptr_t)tokens & 7))
+    return fail(SAE_EINVAL, "tokens_fwd: cls / pos / x need 16-byte, tokens 8-byte alignment");
+  const long long total = (long long)B * (L + 1) * (E / 4);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(tokens_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const __bf16*>(tokens), cls, pos, x, B, L, E);
+  return check_launch("tokens_fwd");
+}
+
+int sae_tokens_bwd(void* stream, int32_t B, int32_t L, int32_t E, const float* dx, void* dtokens, float* dcls,
+                   float* dpos) {
+  if (int rc = tokens_check(B, L, E)) return rc;
+  if (!dx || !dtokens || !dpos) return fail(SAE_EINVAL, "tokens_bwd: NULL argument");
+  if (!aligned16(dx) || !aligned16(dpos) || (dcls && !aligned16(dcls)) || ((uintptr_t)dtokens & 7))
+    return fail(SAE_EINVAL, "tokens_bwd: dx / dcls / dpos need 16-byte, dtokens 8-byte alignment");
+  const int E4 = E / 4;
+  const int G = std::max(1, std::min(B, 512 / E4));
+  const size_t lds = (size_t)G * E4 * 16;
+  if (int rc = lds_attr((const void*)tokens_bwd_kernel, lds)) return rc;
+  hipLaunchKernelGGL(tokens_bwd_kernel, dim3((unsigned)(L + 1)), dim3((unsigned)(G * E4)), lds, (hipStream_t)stream,
+                     dx, reinterpret_cast<__bf16*>(dtokens), dcls, dpos, B, L, E);
+  return check_launch("tokens_bwd");
 }
 
 // ------------------------------------------------------------------ training loss

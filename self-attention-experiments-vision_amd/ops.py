@@ -1117,3 +1117,80 @@ def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, alpha: fl
     if logits.dim() != 2 or logits.stride(1) != 1:
         logits = logits.reshape(-1, logits.shape[-1]).contiguous()
     return _SmoothedCE.apply(logits, labels.to(torch.int64).contiguous(), alpha)
+
+
+# ------------------------------------------------------------------------ encoder input tokens
+class _EncoderTokens(torch.autograd.Function):
+    """concat(cls, float(tokens)) + pos (models/vit.py:82-85,46; position_embed.py:48) in one HIP
+    pass each way (sae_tokens_fwd / _bwd); cls / pos gradients go into their sinks when the
+    multi-rank step registered them."""
+
+    @staticmethod
+    def forward(ctx, tokens, cls, pos):
+        lib = L.load()
+        B, Lt, E = tokens.shape
+        x = torch.empty((B, Lt + 1, E), dtype=torch.float32, device=tokens.device)
+        L.check(lib.sae_tokens_fwd(_stream(tokens), B, Lt, E, _ptr(tokens), _ptr(cls), _ptr(pos), _ptr(x)))
+        ctx.shape = (B, Lt, E)
+        ctx.sinks = (_sink(cls), _sink(pos))
+        ctx.meta = (cls.shape, pos.shape)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        lib = L.load()
+        B, Lt, E = ctx.shape
+        dx = _f32c(dx, "dx")
+        dtok = torch.empty((B, Lt, E), dtype=torch.bfloat16, device=dx.device)
+        scls, spos = ctx.sinks
+        dcls = _claim(scls) if scls is not None else torch.empty(ctx.meta[0], dtype=torch.float32, device=dx.device)
+        dpos = _claim(spos) if spos is not None else torch.empty(ctx.meta[1], dtype=torch.float32, device=dx.device)
+        L.check(lib.sae_tokens_bwd(_stream(dx), B, Lt, E, _ptr(dx), _ptr(dtok), _ptr(dcls), _ptr(dpos)))
+        return dtok, _unsunk(dcls, scls), _unsunk(dpos, spos)
+
+
+def encoder_tokens_ok(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> bool:
+    """Inputs sae_tokens_fwd takes: bf16 [B, L, E] tokens, fp32 contiguous cls [.., E] and pos [1, L+1, E]."""
+    if not (tokens.is_cuda and tokens.dtype == torch.bfloat16 and tokens.dim() == 3 and tokens.is_contiguous()):
+        return False
+    B, Lt, E = tokens.shape
+    return (E % 4 == 0 and E <= 4096 and tokens.data_ptr() % 8 == 0
+            and cls.dtype == torch.float32 and cls.is_contiguous() and cls.numel() == E and cls.data_ptr() % 16 == 0
+            and pos.dtype == torch.float32 and pos.is_contiguous() and pos.numel() == (Lt + 1) * E
+            and pos.data_ptr() % 16 == 0)
+
+
+def encoder_tokens(tokens: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    """fp32 [B, L+1, E] encoder input = concat(cls, float(tokens)) + pos (see _EncoderTokens)."""
+    _require_gpu(tokens, cls, pos)
+    if not encoder_tokens_ok(tokens, cls, pos):
+        raise ValueError("encoder_tokens: needs bf16 contiguous tokens [B, L, E] (E % 4 == 0) and fp32 "
+                         "contiguous cls [E] / pos [L+1, E]")
+    return _EncoderTokens.apply(tokens, cls, pos)
+
+
+class _LayerNormPass(torch.autograd.Function):
+    """(x, LN(x)): the encoder's first LayerNorm, returning its input as the residual stream so that
+    the backward adds the residual gradient in the LayerNorm backward kernel (dx = dxout + LN'^T dy)
+    instead of autograd summing the two paths in a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        _, y, mean, rstd = _ln_fwd(x, None, gamma, beta, eps)
+        ctx.save_for_backward(x, mean, rstd, gamma)
+        ctx.sinks = (_sink(gamma), _sink(beta))
+        return x, y
+
+    @staticmethod
+    def backward(ctx, dxout, dy):
+        x, mean, rstd, gamma = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros(x.shape, dtype=torch.bfloat16, device=x.device)
+        dx, _, dg, db = _ln_bwd(x, mean, rstd, gamma, dy, dxout, False, ctx.sinks)
+        return dx, _unsunk(dg, ctx.sinks[0]), _unsunk(db, ctx.sinks[1]), None
+
+
+def layer_norm_pass(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = LN_EPS):
+    """(x, LayerNorm(x)) -- see _LayerNormPass."""
+    _require_gpu(x, gamma, beta)
+    return _LayerNormPass.apply(x, gamma, beta, eps)

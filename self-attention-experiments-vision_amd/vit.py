@@ -115,8 +115,9 @@ class Encoder(nn.Module):
         self.num_layers = num_layers
         self.LayerNorm_0 = LayerNorm(dim, device)
 
-    def forward(self, inputs, is_training):
-        x = inputs.float() + self.AddAbsPosEmbed_0.pos_embed
+    def forward(self, inputs, is_training, pos_added: bool = False):
+        """``pos_added``: ``inputs`` already hold the position embedding (ops.encoder_tokens)."""
+        x = inputs if pos_added else inputs.float() + self.AddAbsPosEmbed_0.pos_embed
         blocks = [getattr(self, f"EncoderBlock_{i}") for i in range(self.num_layers)]
         if self.dtype == torch.bfloat16 and blocks and ops.layer_norm_ok(x):
             # Same math as vit.py:19-31,57, with every residual add fused into the LayerNorm that
@@ -124,7 +125,8 @@ class Encoder(nn.Module):
             # Dense kernel of the encoder cast to bf16 in one launch up front.
             ops.cast_weights(encoder_weight_groups(blocks))
             try:
-                h = ops.layer_norm(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
+                # (x, h): the residual gradient is added inside the LayerNorm backward kernel
+                x, h = ops.layer_norm_pass(x, blocks[0].LayerNorm_0.scale, blocks[0].LayerNorm_0.bias)
                 for i, blk in enumerate(blocks):
                     a = blk.SelfAttentionBlock_0(h, is_training=is_training)
                     x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
@@ -178,8 +180,13 @@ class ViT(nn.Module):
         """``layout`` "HWCN": ``inputs`` is the train-step feed [H, W, C, B] (train.py:80)."""
         x = patch_tokens(self.PatchEmbedBlock_0, inputs, self.patch_shape, self.dtype, layout)
         b = x.shape[0]
-        x = torch.cat([self.cls.expand(b, 1, self.embed_dim), x.float()], dim=1)   # fp32 (promotion)
-        x = self.Encoder_0(x, is_training)
+        pos = self.Encoder_0.AddAbsPosEmbed_0.pos_embed
+        if self.dtype == torch.bfloat16 and ops.encoder_tokens_ok(x, self.cls, pos):
+            # concat(cls, tokens) + pos_embed into the fp32 residual stream in one pass
+            x = self.Encoder_0(ops.encoder_tokens(x, self.cls, pos), is_training, pos_added=True)
+        else:
+            x = torch.cat([self.cls.expand(b, 1, self.embed_dim), x.float()], dim=1)   # fp32 (promotion)
+            x = self.Encoder_0(x, is_training)
         return self.Dense_0(x[:, 0], self.dtype)
 
 
