@@ -1194,3 +1194,36 @@ def layer_norm_pass(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, ep
     """(x, LayerNorm(x)) -- see _LayerNormPass."""
     _require_gpu(x, gamma, beta)
     return _LayerNormPass.apply(x, gamma, beta, eps)
+
+
+class _ClsAddLayerNorm(torch.autograd.Function):
+    """LayerNorm(x[:, 0] + delta[:, 0]) -> bf16 [B, E]: the encoder's final residual add and
+    LayerNorm on the class-token rows only (ViT's head reads token 0, vit.py:95; the LayerNorm is
+    row-wise, so those rows' values equal the full pass's).  The backward writes the class rows of
+    dx (fp32) and ddelta (bf16); the other rows take no gradient from here."""
+
+    @staticmethod
+    def forward(ctx, x, delta, gamma, beta, eps):
+        xout, y, mean, rstd = _ln_fwd(x[:, 0], delta[:, 0], gamma, beta, eps)
+        ctx.save_for_backward(xout, mean, rstd, gamma)
+        ctx.meta = (x.shape, delta.dtype)
+        ctx.sinks = (_sink(gamma), _sink(beta))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xout, mean, rstd, gamma = ctx.saved_tensors
+        shape, ddt = ctx.meta
+        dxc, ddc, dg, db = _ln_bwd(xout, mean, rstd, gamma, dy, None, True, ctx.sinks)
+        dx = torch.zeros(shape, dtype=torch.float32, device=dxc.device)
+        dx[:, 0] = dxc
+        dd = torch.zeros(shape, dtype=ddt, device=dxc.device)
+        dd[:, 0] = ddc
+        return dx, dd, _unsunk(dg, ctx.sinks[0]), _unsunk(db, ctx.sinks[1]), None
+
+
+def cls_add_layer_norm(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                       eps: float = LN_EPS) -> torch.Tensor:
+    """bf16 LayerNorm(x[:, 0] + delta[:, 0]) of the [B, N, E] residual stream -- see _ClsAddLayerNorm."""
+    _require_gpu(x, delta, gamma, beta)
+    return _ClsAddLayerNorm.apply(x, delta, gamma, beta, eps)

@@ -115,8 +115,10 @@ class Encoder(nn.Module):
         self.num_layers = num_layers
         self.LayerNorm_0 = LayerNorm(dim, device)
 
-    def forward(self, inputs, is_training, pos_added: bool = False):
-        """``pos_added``: ``inputs`` already hold the position embedding (ops.encoder_tokens)."""
+    def forward(self, inputs, is_training, pos_added: bool = False, cls_only: bool = False):
+        """``pos_added``: ``inputs`` already hold the position embedding (ops.encoder_tokens).
+        ``cls_only``: return only token 0 of the normalised output, [B, E] (what ViT's head reads,
+        vit.py:95): the final residual add and LayerNorm (row-wise) then run on those rows only."""
         x = inputs if pos_added else inputs.float() + self.AddAbsPosEmbed_0.pos_embed
         blocks = [getattr(self, f"EncoderBlock_{i}") for i in range(self.num_layers)]
         if self.dtype == torch.bfloat16 and blocks and ops.layer_norm_ok(x):
@@ -131,14 +133,20 @@ class Encoder(nn.Module):
                     a = blk.SelfAttentionBlock_0(h, is_training=is_training)
                     x, h = ops.add_layer_norm(x, a, blk.LayerNorm_1.scale, blk.LayerNorm_1.bias)
                     f = blk.FFBlock_0(h, self.dtype)
-                    nxt = blocks[i + 1].LayerNorm_0 if i + 1 < len(blocks) else self.LayerNorm_0
-                    x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+                    if i + 1 < len(blocks):
+                        nxt = blocks[i + 1].LayerNorm_0
+                        x, h = ops.add_layer_norm(x, f, nxt.scale, nxt.bias)
+                    elif cls_only:
+                        h = ops.cls_add_layer_norm(x, f, self.LayerNorm_0.scale, self.LayerNorm_0.bias)
+                    else:
+                        x, h = ops.add_layer_norm(x, f, self.LayerNorm_0.scale, self.LayerNorm_0.bias)
             finally:
                 ops.clear_weight_cache()
             return h
         for blk in blocks:
             x = blk(x, is_training)
-        return self.LayerNorm_0(x, self.dtype)
+        y = self.LayerNorm_0(x, self.dtype)
+        return y[:, 0] if cls_only else y
 
 
 def patch_tokens(pe: nn.Module, inputs: torch.Tensor, patch_shape: Tuple[int, int], dtype: torch.dtype,
@@ -183,11 +191,11 @@ class ViT(nn.Module):
         pos = self.Encoder_0.AddAbsPosEmbed_0.pos_embed
         if self.dtype == torch.bfloat16 and ops.encoder_tokens_ok(x, self.cls, pos):
             # concat(cls, tokens) + pos_embed into the fp32 residual stream in one pass
-            x = self.Encoder_0(ops.encoder_tokens(x, self.cls, pos), is_training, pos_added=True)
+            x = self.Encoder_0(ops.encoder_tokens(x, self.cls, pos), is_training, pos_added=True, cls_only=True)
         else:
             x = torch.cat([self.cls.expand(b, 1, self.embed_dim), x.float()], dim=1)   # fp32 (promotion)
-            x = self.Encoder_0(x, is_training)
-        return self.Dense_0(x[:, 0], self.dtype)
+            x = self.Encoder_0(x, is_training, cls_only=True)
+        return self.Dense_0(x, self.dtype)   # the class token (vit.py:95-98)
 
 
 # name -> (layers, heads, embed_dim, patch); create_model.py:10-37 plus the DeiT entries (survey D10)

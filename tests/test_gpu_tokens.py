@@ -46,3 +46,27 @@ def test_layer_norm_pass_residual_gradient(dev):
     ((xb * w).sum() + (hb.float() * dy).sum()).backward()
     err = float((xa.grad - xb.grad).abs().max() / xb.grad.abs().max())
     assert err <= 1e-6, err
+
+
+def test_cls_add_layer_norm_matches_full(dev):
+    """The final residual add + LayerNorm on the class-token rows only equals the full pass's token 0
+    (bit-exact forward: the LayerNorm is row-wise); gradients agree with autograd through the full
+    pass to fp32 summation order."""
+    from sae_vision_amd import ops
+    g = torch.Generator(device=dev).manual_seed(9)
+    B, N, E = 4, 197, 384
+    x = torch.randn(B, N, E, device=dev, generator=g)
+    f = torch.randn(B, N, E, device=dev, generator=g).to(torch.bfloat16)
+    gamma = (1 + 0.1 * torch.randn(E, device=dev, generator=g)).requires_grad_(True)
+    beta = (0.1 * torch.randn(E, device=dev, generator=g)).requires_grad_(True)
+    dy = torch.randn(B, E, device=dev, generator=g).to(torch.bfloat16)
+    xa, fa = x.clone().requires_grad_(True), f.clone().requires_grad_(True)
+    xb, fb = x.clone().requires_grad_(True), f.clone().requires_grad_(True)
+    ga, ba = gamma.detach().clone().requires_grad_(True), beta.detach().clone().requires_grad_(True)
+    ha = ops.cls_add_layer_norm(xa, fa, ga, ba)
+    hb = ops.add_layer_norm(xb, fb, gamma, beta)[1][:, 0]
+    assert ha.shape == (B, E) and torch.equal(ha, hb)
+    (ha.float() * dy.float()).sum().backward()
+    (hb.float() * dy.float()).sum().backward()
+    for a, b in ((xa.grad, xb.grad), (fa.grad.float(), fb.grad.float()), (ga.grad, gamma.grad), (ba.grad, beta.grad)):
+        assert float((a - b).abs().max()) <= 1e-6 * max(1.0, float(b.abs().max())), float((a - b).abs().max())
