@@ -200,9 +200,31 @@ class TrainStep:
     # ---- pieces of one step
     def _zero_grad(self):
         if self.flat:
-            self._flat.zero_()
+            ranges = getattr(self, "_zero_ranges", None)
+            if ranges is None:
+                self._flat.zero_()
+            else:   # only the gradients autograd accumulates (every sink is overwritten)
+                for lo, hi in ranges:
+                    self._flat[lo:hi].zero_()
         else:
             self.opt.zero_grad(set_to_none=True)
+
+    def _note_sunk(self):
+        """After a graph-mode backward: the flat ranges of the parameters whose gradients did NOT
+        go through a sink (autograd adds into those, so they need zeroing before the next
+        backward).  Graph mode only: the captured step writes the same sinks on every replay."""
+        from . import ops
+        written = set(ops._SINK_WRITTEN)
+        ranges, off = [], 0
+        for p in self._params:
+            n = p.numel()
+            if p.grad is None or p.grad.data_ptr() not in written:
+                if ranges and ranges[-1][1] == off:
+                    ranges[-1] = (ranges[-1][0], off + n)
+                else:
+                    ranges.append((off, off + n))
+            off += n
+        self._zero_ranges = ranges
 
     def _fwd_bwd(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         self._zero_grad()
@@ -217,6 +239,8 @@ class TrainStep:
         # world > 1: the SUM all-reduce of the per-rank gradients of loss / world is the
         # gradient of the global-batch mean (survey D9)
         (loss / self.world if self.world > 1 else loss).backward()
+        if self.flat and self._sinks and self.graph and not torch.cuda.is_current_stream_capturing():
+            self._note_sunk()
         return loss.detach()
 
     def _allreduce(self):

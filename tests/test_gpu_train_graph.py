@@ -9,15 +9,19 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_graph_step_matches_eager(dev, split):
-    """The graph step (flat gradient buffer with in-place sinks, one-launch FusedAdamW) against the
-    round-1 eager step (autograd's per-parameter gradients, torch's AdamW); split=True: the
-    multi-rank structure (forward + backward graph, the all-reduce point, optimizer graph) at
-    world 1."""
-    from sae_vision_amd import train, vit
+@pytest.mark.parametrize("model,split", [("deit_ti_patch16", False), ("deit_ti_patch16", True), ("cait", False)])
+def test_graph_step_matches_eager(dev, model, split):
+    """The graph step (flat gradient buffer with in-place sinks, only the non-sunk gradient ranges
+    zeroed between replays, one-launch FusedAdamW) against the round-1 eager step (autograd's
+    per-parameter gradients, torch's AdamW); split=True: the multi-rank structure (forward +
+    backward graph, the all-reduce point, optimizer graph) at world 1; CaiT: parameters whose
+    gradients autograd still accumulates (class token, position embedding) beside sunk ones."""
+    from sae_vision_amd import cait, train, vit
     torch.manual_seed(0)
-    m_e = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
+    if model == "cait":
+        m_e = cait.create_cait("cait_xxs_24", 1000, torch.bfloat16, stoch_depth=False, device=dev)
+    else:
+        m_e = vit.create_model(model, 1000, torch.bfloat16, device=dev)
     m_g = copy.deepcopy(m_e)
     s_e = train.TrainStep(m_e, global_batch=8, device=dev, flat_grads=False)
     s_g = train.TrainStep(m_g, global_batch=8, device=dev, graph=True, two_graphs=split)
@@ -35,6 +39,7 @@ def test_graph_step_matches_eager(dev, split):
         lg.append(float(s_g(x, y)))
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
+    assert s_g._zero_ranges is not None   # graph mode zeroes only what autograd accumulates
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         err = float((pe - pg).abs().max())
         assert err <= 1e-3 * max(1.0, float(pe.abs().max())), (n, err)
