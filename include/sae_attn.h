@@ -316,13 +316,14 @@ int sae_tokens_bwd(void* stream, int32_t B, int32_t L, int32_t E, const float* d
      loss = mean_r [ lse_r - (1 - alpha) x[r, labels[r]] - (alpha / classes) sum_c x[r, c] ]
    logits x [rows][classes] (row stride ld elements, dtype SAE_DTYPE_BF16 or SAE_DTYPE_F32),
    labels int64 [rows] (a label outside [0, classes) contributes no target term).  fwd writes
-   lse [rows] (fp32, for the backward) and *loss (fp32, device memory); the row losses are summed
-   in row order (deterministic).  bwd writes dlogits [rows][classes] (row stride ldd, the logits'
+   lse [rows] (fp32, for the backward), row_loss [rows] (fp32) and *loss (fp32, device memory);
+   the row losses are summed in a fixed order (deterministic).  bwd writes dlogits [rows][classes] (row stride ldd, the logits'
    dtype) = (*grad_loss / rows) (softmax(x_r) - (1 - alpha) onehot - alpha / classes).
    rows <= SAE_CE_MAX_ROWS. */
 #define SAE_CE_MAX_ROWS 16384
 int sae_smoothed_ce_fwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
-                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* loss);
+                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* row_loss,
+                        float* loss);
 int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
                         int32_t dtype, const int64_t* labels, float alpha, const float* lse,
                         const float* grad_loss, void* dlogits, int64_t ldd);

@@ -1349,21 +1349,19 @@ static int ce_check(int32_t rows, int32_t classes, const void* logits, int64_t l
 }
 
 int sae_smoothed_ce_fwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,
-                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* loss) {
+                        int32_t dtype, const int64_t* labels, float alpha, float* lse, float* row_loss, float* loss) {
   if (int rc = ce_check(rows, classes, logits, ld, dtype, labels)) return rc;
-  if (!lse || !loss) return fail(SAE_EINVAL, "smoothed_ce_fwd: NULL lse / loss");
+  if (!lse || !row_loss || !loss) return fail(SAE_EINVAL, "smoothed_ce_fwd: NULL lse / row_loss / loss");
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)rows * 4;
-  if (dtype == SAE_DTYPE_BF16) {
-    if (int rc = lds_attr((const void*)smoothed_ce_fwd_kernel<__bf16>, lds)) return rc;
-    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<__bf16>, dim3(1), dim3(64 * kCeWaves), lds, st,
-                       reinterpret_cast<const __bf16*>(logits), (long long)ld, labels, rows, classes, alpha, lse, loss);
-  } else {
-    if (int rc = lds_attr((const void*)smoothed_ce_fwd_kernel<float>, lds)) return rc;
-    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<float>, dim3(1), dim3(64 * kCeWaves), lds, st,
-                       reinterpret_cast<const float*>(logits), (long long)ld, labels, rows, classes, alpha, lse, loss);
-  }
-  return check_launch("smoothed_ce_fwd");
+  if (dtype == SAE_DTYPE_BF16)
+    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<__bf16>, dim3(rows), dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(logits), (long long)ld, labels, classes, alpha, lse, row_loss);
+  else
+    hipLaunchKernelGGL(smoothed_ce_fwd_kernel<float>, dim3(rows), dim3(256), 0, st,
+                       reinterpret_cast<const float*>(logits), (long long)ld, labels, classes, alpha, lse, row_loss);
+  if (int rc = check_launch("smoothed_ce_fwd")) return rc;
+  hipLaunchKernelGGL(smoothed_ce_mean_kernel, dim3(1), dim3(256), 0, st, row_loss, rows, loss);
+  return check_launch("smoothed_ce_mean");
 }
 
 int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void* logits, int64_t ld,

@@ -1083,7 +1083,7 @@ def add_layer_norm(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, be
 # ------------------------------------------------------------------------------ training loss
 class _SmoothedCE(torch.autograd.Function):
     """Label-smoothed softmax cross entropy, mean over rows (train.py:77-90: optax.smooth_labels +
-    jnp.mean(optax.softmax_cross_entropy)) in two HIP launches (sae_smoothed_ce_fwd / _bwd);
+    jnp.mean(optax.softmax_cross_entropy)) in three HIP launches (sae_smoothed_ce_fwd / _bwd);
     dlogits come back in the logits' dtype."""
 
     @staticmethod
@@ -1091,9 +1091,10 @@ class _SmoothedCE(torch.autograd.Function):
         lib = L.load()
         R, K = logits.shape
         lse = torch.empty(R, dtype=torch.float32, device=logits.device)
+        row_loss = torch.empty(R, dtype=torch.float32, device=logits.device)
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         L.check(lib.sae_smoothed_ce_fwd(_stream(logits), R, K, _ptr(logits), logits.stride(0), dtype_code(logits.dtype),
-                                        _ptr(labels), float(alpha), _ptr(lse), _ptr(loss)))
+                                        _ptr(labels), float(alpha), _ptr(lse), _ptr(row_loss), _ptr(loss)))
         ctx.save_for_backward(logits, labels, lse)
         ctx.alpha = float(alpha)
         return loss
