@@ -1218,7 +1218,10 @@ int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* i
       c.ld16 = s.ld16;
       c.ldT = s.ldT;
       c.col0 = s.col0;
-      c.tiles = ((s.K + 31) / 32) * ((s.N + 31) / 32);
+      const auto a8 = [](const void* p) { return ((uintptr_t)p & 7) == 0; };
+      c.vec = s.K % 4 == 0 && s.N % 4 == 0 && s.col0 % 4 == 0 && aligned16(s.w) &&
+              (!s.w16 || (s.ld16 % 4 == 0 && a8(s.w16))) && (!s.wt16 || (s.ldT % 4 == 0 && a8(s.wt16)));
+      c.tiles = c.vec ? ((s.K + 63) / 64) * ((s.N + 63) / 64) : ((s.K + 31) / 32) * ((s.N + 31) / 32);
       tiles += c.tiles;
     }
     if (tiles >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "weight_cast_multi: too many tiles");

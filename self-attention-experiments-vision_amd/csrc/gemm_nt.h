@@ -310,25 +310,63 @@ __global__ __launch_bounds__(256) void weight_cast_kernel(const float* w, __bf16
 
 // Every Dense kernel of a model cast in ONE launch (the per-weight casts are ~4 us each, almost
 // all launch / ramp latency): item i casts w_i [K][N] into columns col0 .. col0 + N of
-// w16 [K][ld16] and rows col0 .. col0 + N of wt16 [*][ldT]; 32 x 32 tiles, items located by a
-// prefix sum over their tile counts.
+// w16 [K][ld16] and rows col0 .. col0 + N of wt16 [*][ldT]; items located by a prefix sum over
+// their tile counts.  Items whose sizes, offsets and pointers allow it (vec) take 64 x 64 tiles
+// with 16-byte loads and 8-byte bf16x4 stores both ways (HBM-bound: 4 B read + 2 x 2 B written
+// per element); the others 32 x 32 tiles element by element.
 constexpr int kCastMax = 48;
 struct CastItem {
   const float* w;
   __bf16* w16;
   __bf16* wt16;
-  int K, N, ld16, ldT, col0, tiles;
+  int K, N, ld16, ldT, col0, tiles, vec;
 };
 struct CastList {
   CastItem it[kCastMax];
   int n;
 };
 
+__device__ __forceinline__ void cast_tile_vec(const CastItem& c, int b, float (*tile)[65]) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  const int tn = (c.N + 63) / 64;
+  const int k0 = (b / tn) * 64, n0 = (b % tn) * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = t + 256 * q, row = i >> 4, c4 = i & 15;
+    const int k = k0 + row, n = n0 + 4 * c4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (k < c.K && n < c.N) {
+      v = *reinterpret_cast<const f32x4*>(c.w + (long long)k * c.N + n);
+      if (c.w16)
+        *reinterpret_cast<bf16x4*>(c.w16 + (long long)k * c.ld16 + c.col0 + n) =
+            bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[row][4 * c4 + e] = v[e];
+  }
+  if (!c.wt16) return;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = t + 256 * q, nn = i >> 4, kk = i & 15;
+    const int n = n0 + nn, k = k0 + 4 * kk;
+    if (n < c.N && k < c.K)
+      *reinterpret_cast<bf16x4*>(c.wt16 + (long long)(c.col0 + n) * c.ldT + k) =
+          bf16x4{(__bf16)tile[4 * kk][nn], (__bf16)tile[4 * kk + 1][nn], (__bf16)tile[4 * kk + 2][nn],
+                 (__bf16)tile[4 * kk + 3][nn]};
+  }
+}
+
 __global__ __launch_bounds__(256) void weight_cast_multi_kernel(CastList L) {
-  __shared__ float tile[32][33];
+  __shared__ float tile[64][65];
   int b = blockIdx.x, i = 0;
   while (i + 1 < L.n && b >= L.it[i].tiles) b -= L.it[i++].tiles;
   const CastItem& c = L.it[i];
+  if (c.vec) {
+    cast_tile_vec(c, b, tile);
+    return;
+  }
   const int tn = (c.N + 31) / 32;
   const int k0 = (b / tn) * 32, n0 = (b % tn) * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;

@@ -187,6 +187,8 @@ def test_cast_weights_multi_exact(dev):
     wo = torch.randn(H, D, C, device=dev, generator=g)
     ws = [[w.reshape(C, H * D) for w in (wq, wk, wv)], [wo.reshape(H * D, C)]]
     ws += [[torch.randn(96, 40, device=dev, generator=g)] for _ in range(60)]   # > one launch of items
+    ws += [[torch.randn(30, 37, device=dev, generator=g)], [torch.randn(130, 68, device=dev, generator=g)]]
+    # (30 x 37: the element-wise 32 x 32 path; 130 x 68: 64 x 64 vector tiles with ragged edges)
     ops.cast_weights(ws)
     try:
         w16, wt16 = ops._cast_lookup(ws[0])
