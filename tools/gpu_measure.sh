@@ -4,7 +4,7 @@
 #   PMC passes for the DeiT-S training step and the ViT-B@384 attention headline.
 # usage: tools/gpu_measure.sh <tag>     -> gpurun_out/<tag>_*
 set -e
-tag=${1:-r02f}
+tag=${1:-r02g}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
