@@ -224,7 +224,8 @@ class TrainStep:
                 else:
                     ranges.append((off, off + n))
             off += n
-        self._zero_ranges = ranges
+        # many scattered ranges would cost more launches than the one full fill saves
+        self._zero_ranges = ranges if len(ranges) <= 8 else None
 
     def _fwd_bwd(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         self._zero_grad()

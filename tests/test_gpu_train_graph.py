@@ -39,7 +39,8 @@ def test_graph_step_matches_eager(dev, model, split):
         lg.append(float(s_g(x, y)))
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
-    assert s_g._zero_ranges is not None   # graph mode zeroes only what autograd accumulates
+    if model != "cait":   # every ViT parameter has a sink: nothing left to zero between replays
+        assert s_g._zero_ranges == []
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         err = float((pe - pg).abs().max())
         assert err <= 1e-3 * max(1.0, float(pe.abs().max())), (n, err)
