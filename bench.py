@@ -1,24 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: DeiT-S/16 224px bf16 data-parallel training on MI355X (BASELINE.json configs[1]
-at N=1, configs[2]-style DP scaling at N>1) with the fused HIP attention on the hot path.
+at N=1; the same per-GPU workload at N>1, weak scaling) with the fused HIP attention on the hot path.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-One process per GPU; the batch (128 images per GPU, synthetic N(0,1) images + uniform labels,
-resident in HBM) is sharded across ranks, gradients are all-reduced over RCCL (DDP buckets
-overlapped with the backward); at N=1 the whole step (forward, loss, backward, AdamW) is one HIP
-graph, replayed (--eager: launch it op by op).  W untimed warm-up steps, then exactly K steps
-bracketed by a barrier + device synchronisation on both sides; the max elapsed time over ranks is
-used.
+One process per GPU; each rank holds 128 synthetic N(0,1) images (fed as the reference's train step
+receives them: HWCN fp32, train.py:80-81) + uniform labels, resident in HBM.  The step is forward,
+smoothed cross-entropy, backward and AdamW, replayed as ONE HIP graph (train.TrainStep): every
+gradient is written in place into a flat fp32 buffer, and at N>1 each ~25 MB bucket of it is
+all-reduced on RCCL (backend nccl) on a communication stream as soon as its last gradient is
+written, inside the captured backward (overlapped with the rest of it; the compute stream joins
+before AdamW).  ``--world1-rccl`` runs that collective path at N=1 with a one-rank RCCL group;
+``--two-graphs`` puts the all-reduce between a forward+backward graph and an AdamW graph;
+``--eager`` launches the step op by op.  W untimed warm-up steps, then exactly K steps bracketed
+by a barrier + device synchronisation on both sides; the max elapsed time over ranks is used.
 Rank 0 prints ONE JSON line:
   value        = whole-job training images/s (all ranks)
-  roofline     = the fused attention op of this workload (fwd + bwd = 3 launches: attn_fwd,
-                 attn_bwd_dq (+ delta), attn_bwd_dkdv), timed live with HIP events on its launch
-                 stream inside the timed region (graph mode: over 3 eager steps right after it,
-                 since graph replays carry no host events); algorithmic FLOPs/bytes per call
-                 (DESIGN.md §4);
-                 traffic = HBM bytes per call from profiles/pmc_traffic.json (rocprofv3 PMC)
+  roofline     = the fused attention op of this workload: one call = 2 launches (attn_fwd2 +
+                 the single-pass attn_bwd3 at DeiT-S), timed with HIP events on the launch stream
+                 around a HIP graph of 10 back-to-back calls at the workload's layer shape (packed
+                 [B, N, 3, H, D] q/k/v), median of 20 replays, after the timed region (events
+                 inside a captured step cannot be read); algorithmic FLOPs / bytes per call
+                 (DESIGN.md §4); traffic = HBM bytes per call from profiles/pmc_traffic.json
+                 (rocprofv3 PMC, gfx950 FETCH_SIZE correction)
   cpu_baseline = the numpy port (oracle/vit_ref.py) of the same training step on a bounded
                  sample, on this host's cores (rank 0, N=1 only); .configs0 = BASELINE configs[0]
                  (DeiT-Ti forward + loss, batch 8); .attention = the unfused attention core fwd+bwd
@@ -231,6 +236,19 @@ def headline(dev, iters=20, reps=10, f32=False):
             "timing": f"HIP graphs of {reps} launches, median of {iters} replays", "roofline": r}
 
 
+def step_label(step, use_graph):
+    """What the timed step ran, named by the collective path that actually executed (train.py)."""
+    if not (use_graph and step.graph):
+        base = "eager"
+    elif step.two_graphs:
+        base = "hip_graphs(fwd+bwd, adamw)"
+    else:
+        base = "hip_graph_replay"
+    coll = {"none": "no collective", "overlap": "rccl_allreduce overlapped with the backward",
+            "between": "rccl_allreduce between the graphs", "host": "gloo host all-reduce between the graphs"}
+    return f"{base} + {coll[step.collective]}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,7 +274,13 @@ def main():
                          "input_pipeline.py:187-191), gathered by the fused patch GEMM; NHWC: the model call")
     ap.add_argument("--no-grad-sinks", action="store_true",
                     help="flat gradient buffer without the in-place gradient sinks (autograd adds into it)")
+    ap.add_argument("--world1-rccl", action="store_true",
+                    help="N=1: a one-rank RCCL process group, so the overlapped bucket all-reduces run (captured "
+                         "in the step's HIP graph) as they do at N > 1")
+    ap.add_argument("--bucket-mb", type=float, default=25.0, help="gradient all-reduce bucket size")
     args = ap.parse_args()
+    if args.world1_rccl:
+        os.environ["SAE_WORLD1_RCCL"] = "1"
 
     import torch
     import torch.distributed as dist
@@ -276,12 +300,12 @@ def main():
     else:
         model = vit.create_model(args.model, 1000, torch.bfloat16, img_size=args.img_size, device=dev)
     B = args.batch
-    # N = 1: the whole step (forward, loss, backward, AdamW) replayed as one HIP graph; N > 1:
-    # forward + backward graph, bucketed RCCL all-reduce of the flat gradient, AdamW graph
+    # the whole step (forward, loss, backward with the overlapped bucket all-reduces at N > 1, AdamW)
+    # replayed as one HIP graph
     use_graph = not args.eager
     step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph, input_layout=args.input_layout,
                            flat_grads=False if args.no_flat_grads else None, grad_sinks=not args.no_grad_sinks,
-                           two_graphs=True if args.two_graphs else None)
+                           two_graphs=True if args.two_graphs else None, bucket_cap_mb=args.bucket_mb)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
     if args.input_layout == "HWCN":
@@ -367,9 +391,9 @@ def main():
                    "heads": Hh, "head_dim": D, "layers": L, "parallelism": f"dp{world}",
                    "input": f"{args.input_layout} fp32 images (patch gather fused into the embedding GEMM)",
                    # what actually ran: a capture that failed leaves the step eager (train.py)
-                   "step": ("hip_graph_replay" if not step.two_graphs else
-                            "hip_graphs+" + ("rccl" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend())
-                            + "_allreduce") if use_graph and step.graph else "eager"},
+                   "step": step_label(step, use_graph),
+                   "collective": {"mode": step.collective, "process_group": dist.get_backend() if step.pg else None,
+                                  "buckets": len(getattr(step, "_buckets", [])), "bucket_cap_mb": args.bucket_mb}},
         "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,
         "attention": {"kernel": kf.replace("_fwd", ""), "calls_per_step": ksum[kf]["launches"] // timed_steps,

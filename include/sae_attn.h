@@ -126,8 +126,9 @@ int sae_rotary(void* stream, int32_t batch, int32_t seq, int32_t heads, int32_t 
    (sin/cos fp32 [max(seq_q, seq_k)][head_dim / 2], row = position), so the rotated tensors
    never exist in memory; the backward returns dq / dk for the un-rotated q / k (rotated back
    as they are stored).  Bit-identical to sae_rotary + sae_attn_fwd / sae_attn_bwd + sae_rotary
-   (inverse).  bf16, 16-byte aligned strides, head_dim % 8 == 0 (backward: head_dim <= 64),
-   no flags; otherwise SAE_EUNSUPPORTED (use sae_rotary + the plain entry points). */
+   (inverse).  bf16, 16-byte aligned strides, head_dim % 8 == 0 and head_dim <= 64 (forward
+   and backward alike, so a forward that runs always has its backward), no flags; otherwise
+   SAE_EUNSUPPORTED (use sae_rotary + the plain entry points). */
 int sae_attn_fwd_rotary(void* stream, const sae_attn_desc* desc, const void* q, const void* k,
                         const void* v, const float* sin_tab, const float* cos_tab, void* o,
                         float* lse);

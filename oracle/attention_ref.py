@@ -401,14 +401,14 @@ def _rb(x):
 
 
 def attention_block_bwd_bf16(x_q, x_kv, p: AttnParams, dy):
-    """bf16-emulated JAX autodiff of ``attention_block_fwd(..., "bf16")`` (no talking heads,
-    no rotary): the cotangent of every bf16 value is bf16 (each dot_general / elementwise op of
-    the backward rounds its output; products accumulate in wider precision), the gradient of a
-    bf16-cast fp32 parameter is the bf16 cotangent cast back to fp32.  jax.nn.softmax's VJP
-    (jax 0.2.x) is ``p * (g - sum(g * p))`` evaluated in bf16.  Returns the same keys as
-    :func:`attention_block_bwd`."""
-    if p.th1 is not None or p.th2 is not None:
-        raise NotImplementedError("bf16 chain: talking heads run their mix in fp32 (survey D8)")
+    """bf16-emulated JAX autodiff of ``attention_block_fwd(..., "bf16")`` (no rotary): the
+    cotangent of every bf16 value is bf16 (each dot_general / elementwise op of the backward rounds
+    its output; products accumulate in wider precision), the gradient of a bf16-cast fp32
+    parameter is the bf16 cotangent cast back to fp32.  jax.nn.softmax's VJP (jax 0.2.x) is
+    ``p * (g - sum(g * p))`` evaluated in bf16.  Talking heads (attention.py:44-52): the fp32
+    transforms promote the scores, so the mixes, the softmax, P V and their cotangents are fp32
+    (survey D8) until the bf16 scores' and the bf16-cast output's cotangents.  Returns the same
+    keys as :func:`attention_block_bwd`."""
     y, aux = attention_block_fwd(x_q, x_kv, p, "bf16", return_aux=True)
     f = lambda t: np.asarray(t, np.float64)
     xq, xkv = _rb(x_q), _rb(x_kv)
@@ -418,13 +418,24 @@ def attention_block_bwd_bf16(x_q, x_kv, p: AttnParams, dy):
     D = q.shape[-1]
     g = {}
     dyb = _rb(dy)
-    g["DenseGeneral_0"] = _rb(np.einsum("bnhd,bnc->hdc", o, dyb))
+    g["DenseGeneral_0"] = _rb(np.einsum("bnhd,bnc->hdc", _rb(o), dyb))
     do = _rb(np.einsum("bnc,hdc->bnhd", dyb, Wo))
-    dv = _rb(np.einsum("bhqk,bqhd->bkhd", pr, do))
-    dp = _rb(np.einsum("bqhd,bkhd->bhqk", do, v))
-    t = _rb(dp * pr)
-    sm = _rb(t.sum(-1, keepdims=True))
-    ds = _rb(pr * _rb(dp - sm))
+    if p.th1 is None and p.th2 is None:
+        dv = _rb(np.einsum("bhqk,bqhd->bkhd", pr, do))
+        dp = _rb(np.einsum("bqhd,bkhd->bhqk", do, v))
+        t = _rb(dp * pr)
+        sm = _rb(t.sum(-1, keepdims=True))
+        ds = _rb(pr * _rb(dp - sm))
+    else:
+        t1, t2 = f(p.th1), f(p.th2)
+        p2, s = f(aux["p2"]), f(aux["s"])
+        dv = _rb(np.einsum("bhqk,bqhd->bkhd", p2, do))                      # fp32 P V, bf16-cast v
+        dp2 = np.einsum("bqhd,bkhd->bhqk", do, v)
+        g["TalkingHeadsBlock_1"] = np.einsum("bhqk,biqk->hi", pr, dp2)
+        dp = np.einsum("hi,biqk->bhqk", t2, dp2)
+        ds1 = pr * (dp - (dp * pr).sum(-1, keepdims=True))                    # fp32 softmax VJP
+        g["TalkingHeadsBlock_0"] = np.einsum("bhqk,biqk->hi", s, ds1)
+        ds = _rb(np.einsum("hi,biqk->bhqk", t1, ds1))                         # cotangent of bf16 scores
     dqh = _rb(np.einsum("bhqk,bkhd->bqhd", ds, k))
     dk = _rb(np.einsum("bhqk,bqhd->bkhd", ds, qh))
     dq = _rb(dqh / np.sqrt(D))

@@ -574,14 +574,14 @@ static int attn_fwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
                    strides_vec(d->v_stride, epc) && strides_vec(d->o_stride, epc) && aligned16(q) &&
                    aligned16(k) && aligned16(v) && aligned16(o);
   const int var = dev_knob("SAE_FWD_VARIANT");
-  if (rope) {   // rotary rides on the lean bf16 kernels only
-    if (d->dtype != SAE_DTYPE_BF16 || !vec || rel || d->flags)
-      return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 path (16-byte aligned strides, no flags)");
-    a.rope = *rope;
+  if (rope) {   // rotary rides on the lean bf16 kernels only, in the envelope of sae_attn_bwd_rotary
     const int dp = pick_dp(d->head_dim);
+    if (d->dtype != SAE_DTYPE_BF16 || !vec || rel || d->flags || dp > 64)
+      return fail(SAE_EUNSUPPORTED, "rotary: fused only on the bf16 path with head_dim <= 64 (16-byte aligned "
+                  "strides, no flags)");
+    a.rope = *rope;
     if (dp == 32) return fwd2_dispatch<32, true>((hipStream_t)stream, a, 0);
-    if (dp == 64) return fwd2_dispatch<64, true>((hipStream_t)stream, a, 0);
-    return fwd2_dispatch<128, true>((hipStream_t)stream, a, 0);
+    return fwd2_dispatch<64, true>((hipStream_t)stream, a, 0);
   }
   if (var != 1 && vec && cls_ok(d)) return cls_run<false>((hipStream_t)stream, a);
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {

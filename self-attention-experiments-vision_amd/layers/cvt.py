@@ -75,15 +75,23 @@ class ConvProjectionBlock(nn.Module):
     def forward(self, x, is_training):   # x [b, H, W, c] -> [b, H', W', out]
         dt, k, s = self.dtype, self.kernel_size, self.strides
         c = x.shape[-1]
-        xc = x.to(dt).permute(0, 3, 1, 2)
-        H, W = xc.shape[-2:]
+        xc = x.to(dt)                                                   # [b, H, W, c]
+        H, W = xc.shape[1:3]
         # Flax 'SAME': output ceil(n / s), total padding max((ceil(n/s) - 1) s + k - n, 0), low = total // 2
-        ph = max((math.ceil(H / s) - 1) * s + k - H, 0)
-        pw = max((math.ceil(W / s) - 1) * s + k - W, 0)
-        xc = F.pad(xc, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
-        w0 = self.Conv_0.kernel.to(dt).permute(3, 2, 0, 1)            # [c, 1, k, k]
-        y = F.conv2d(xc, w0, stride=s, groups=c).permute(0, 2, 3, 1)
-        y = self.BatchNorm_0(y, is_training)
+        Ho, Wo = math.ceil(H / s), math.ceil(W / s)
+        ph = max((Ho - 1) * s + k - H, 0)
+        pw = max((Wo - 1) * s + k - W, 0)
+        xp = F.pad(xc.float(), (0, 0, pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+        # the depthwise k x k conv as k^2 strided multiply-adds in fp32 (exact fp32 products and a
+        # fixed summation order; inputs and kernel cast to the compute dtype first, as Flax's Conv
+        # does), output in the compute dtype
+        w0 = self.Conv_0.kernel.to(dt).float()                          # [k, k, 1, c]
+        y = None
+        for i in range(k):
+            for j in range(k):
+                tap = xp[:, i:i + s * (Ho - 1) + 1:s, j:j + s * (Wo - 1) + 1:s, :] * w0[i, j, 0]
+                y = tap if y is None else y + tap
+        y = self.BatchNorm_0(y.to(dt), is_training)
         w1 = self.Conv_1.kernel.reshape(c, -1)                          # [c, out]
         b1 = self.Conv_1.bias
         return ops.dense(y, w1, b1, dt)

@@ -59,6 +59,27 @@ class KernelTimer:
 _TIMER = None
 
 
+def _sinking(bwd):
+    """Backward of an op that may write gradient sinks (the flat DP buffer, see set_grad_sinks):
+    once its kernels are enqueued, report every sink it claimed to the sink listener (the training
+    step launches a gradient bucket's all-reduce as soon as all of the bucket's gradients are
+    written, overlapping it with the rest of the backward)."""
+    import functools
+
+    @functools.wraps(bwd)
+    def wrapped(ctx, *grads):
+        n0 = len(_CLAIM_LOG)
+        out = bwd(ctx, *grads)
+        if len(_CLAIM_LOG) > n0:
+            done = _CLAIM_LOG[n0:]
+            del _CLAIM_LOG[n0:]
+            if _SINK_LISTENER is not None:
+                for ptr in done:
+                    _SINK_LISTENER(ptr)
+        return out
+    return wrapped
+
+
 def set_kernel_timer(t):
     global _TIMER
     _TIMER = t
@@ -186,6 +207,7 @@ class _Attention(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_sinking
     def backward(ctx, do):
         q, k, v, o, lse, bias_h, bias_w = ctx.saved_tensors
         do = _grad_in(do)
@@ -207,6 +229,7 @@ class _AttentionPacked(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_sinking
     def backward(ctx, do):
         qkv, o, lse = ctx.saved_tensors
         do = _grad_in(do)
@@ -304,6 +327,7 @@ class _TalkingHeads(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_sinking
     def backward(ctx, do):
         q, k, v, th1, th2, lse = ctx.saved_tensors
         do = _grad_in(do)
@@ -326,6 +350,7 @@ class _TalkingHeadsPacked(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_sinking
     def backward(ctx, do):
         qkv, th1, th2, lse = ctx.saved_tensors
         do = _grad_in(do)
@@ -385,6 +410,7 @@ class _RelposBias(torch.autograd.Function):
         return bh, bw
 
     @staticmethod
+    @_sinking
     def backward(ctx, dbh, dbw):
         qhat, eh, ew = ctx.saved_tensors
         lib = L.load()
@@ -448,6 +474,7 @@ class _Rotary(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dy):
         dy = _grad_in(dy)
         B, N, H, D = dy.shape
@@ -473,6 +500,9 @@ def rotary(x: torch.Tensor, base: float = 10000.0) -> torch.Tensor:
 # models is applied once per step); a second write raises instead of silently overwriting.
 _GRAD_SINKS = {}      # id(param) -> (weakref(param), fp32 view shaped like the param)
 _SINK_WRITTEN = set()
+_SINK_WINDOW = False  # sinks are used only between begin_backward_sinks() and end_backward_sinks()
+_CLAIM_LOG = []       # data pointers of the sinks claimed by the backward function now running
+_SINK_LISTENER = None  # called with a sink's data pointer once the kernel writing it is enqueued
 
 
 def set_grad_sinks(params, views=None) -> None:
@@ -489,14 +519,33 @@ def set_grad_sinks(params, views=None) -> None:
 
 
 def begin_backward_sinks() -> None:
-    """Start of a step's backward: every sink may be written once again."""
+    """Open the sink window for one backward (the training step's): every sink may be written once
+    again.  Outside the window the ops ignore the sinks and hand autograd ordinary gradients, so a
+    backward outside a training step (gradient accumulation, a manual check) keeps autograd's
+    accumulate semantics."""
+    global _SINK_WINDOW
     _SINK_WRITTEN.clear()
+    del _CLAIM_LOG[:]
+    _SINK_WINDOW = True
+
+
+def end_backward_sinks() -> None:
+    """Close the sink window (the written set stays readable until the next begin)."""
+    global _SINK_WINDOW
+    _SINK_WINDOW = False
+
+
+def set_sink_listener(fn) -> None:
+    """``fn(data_ptr)`` is called for every sink once the kernel that writes it has been enqueued on
+    the current stream (None: no listener)."""
+    global _SINK_LISTENER
+    _SINK_LISTENER = fn
 
 
 def _sink(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     """The sink of parameter ``t`` (or of the parameter ``t`` is a full reshape view of), viewed as
     ``t``'s shape; None when it has none."""
-    if t is None or not t.requires_grad or not _GRAD_SINKS:
+    if t is None or not t.requires_grad or not _GRAD_SINKS or not _SINK_WINDOW:
         return None
     base = t if t._base is None else t._base
     e = _GRAD_SINKS.get(id(base))
@@ -515,6 +564,7 @@ def _claim(sink: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         if key in _SINK_WRITTEN:
             raise RuntimeError("gradient sink written twice in one backward: a parameter feeds two ops")
         _SINK_WRITTEN.add(key)
+        _CLAIM_LOG.append(key)
     return sink
 
 
@@ -629,6 +679,7 @@ class _Dense(torch.autograd.Function):
         return y.view(*x.shape[:-1], J)
 
     @staticmethod
+    @_sinking
     def backward(ctx, dy):
         x2, wd = ctx.saved_tensors
         I, J = wd.shape
@@ -724,6 +775,7 @@ class _PatchEmbed(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_sinking
     def backward(ctx, dout):
         lib = L.load()
         (images,) = ctx.saved_tensors
@@ -865,6 +917,7 @@ class _FFBlock(torch.autograd.Function):
         return y.view(*x.shape[:-1], w1.shape[1])
 
     @staticmethod
+    @_sinking
     def backward(ctx, dy):
         x2, h, a, w0p, w1p = ctx.saved_tensors
         I, Hd = w0p.shape
@@ -980,6 +1033,7 @@ class _LayerNorm(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dy):
         x, mean, rstd, gamma = ctx.saved_tensors
         dx, _, dg, db = _ln_bwd(x, mean, rstd, gamma, dy, None, False, ctx.sinks)
@@ -996,6 +1050,7 @@ class _AddLayerNorm(torch.autograd.Function):
         return xout, y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dxout, dy):
         xout, mean, rstd, gamma = ctx.saved_tensors
         if dy is None:
@@ -1030,6 +1085,7 @@ class _AddLayerNormScaled(torch.autograd.Function):
         return xout, y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dxout, dy):
         xout, mean, rstd, gamma, delta, lsf, rowscale = ctx.saved_tensors
         lib = L.load()
@@ -1100,6 +1156,7 @@ class _SmoothedCE(torch.autograd.Function):
         return loss
 
     @staticmethod
+    @_sinking
     def backward(ctx, gloss):
         lib = L.load()
         logits, labels, lse = ctx.saved_tensors
@@ -1138,6 +1195,7 @@ class _EncoderTokens(torch.autograd.Function):
         return x
 
     @staticmethod
+    @_sinking
     def backward(ctx, dx):
         lib = L.load()
         B, Lt, E = ctx.shape
@@ -1183,6 +1241,7 @@ class _LayerNormPass(torch.autograd.Function):
         return x, y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dxout, dy):
         x, mean, rstd, gamma = ctx.saved_tensors
         if dy is None:
@@ -1212,6 +1271,7 @@ class _ClsAddLayerNorm(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_sinking
     def backward(ctx, dy):
         xout, mean, rstd, gamma = ctx.saved_tensors
         shape, ddt = ctx.meta

@@ -2,15 +2,24 @@
 
 One process per GPU, ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm) over
 xGMI.  The reference's ``jax.pmap(train_step)`` + ``lax.pmean(grads)`` (train.py:94-96,230)
-becomes: every parameter's gradient is a view into ONE flat fp32 buffer; the backward of
-loss / world fills it; the buffer is all-reduced (SUM = the global-batch mean) in a few large
-buckets on RCCL; the fused AdamW steps on the views.  On the GPU the step is GPU-bound by
-construction: forward + loss + backward is one HIP graph, the optimizer a second one, and only
-the bucket all-reduces are launched eagerly between the two replays (a handful of host calls per
-step instead of the ~600 launches of an eager step, whose ~10 ms of host submission matched the
-GPU time).  Survey D9 decisions: standard descent (the reference's optax chain
-ascends), the gradient is the global batch mean (the reference divides the loss by device_count
-*and* pmean's), no wandb call inside the step.
+becomes: every parameter's gradient is a 16-byte-aligned view into ONE flat fp32 buffer, cut
+into buckets along parameter boundaries in the order the backward finishes them; the backward
+kernels write the gradients straight into their views (gradient sinks, ops.set_grad_sinks), and
+as soon as the last gradient of a bucket is written its SUM all-reduce (of the gradients of
+loss / world = the global-batch mean) is launched on a communication stream, overlapping the
+rest of the backward; the compute stream joins that stream before the one-launch AdamW.  On the
+GPU the whole step -- forward, loss, backward with the overlapped bucket all-reduces, AdamW -- is
+ONE HIP graph (RCCL collectives are graph-capturable: tools/probe/rccl_graph.py), so a step costs
+one host call.  Survey D9 decisions: standard descent (the reference's optax chain ascends), the
+gradient is the global batch mean (the reference divides the loss by device_count *and*
+pmean's), no wandb call inside the step.
+
+Collective modes (``TrainStep.collective``): "overlap" (default whenever there is a process group:
+bucket all-reduces launched from inside the backward), "between" (``two_graphs=True``: forward +
+backward graph, the bucket all-reduces, optimizer graph), "host" (gloo with CUDA tensors, the
+multi-rank rehearsal on one GPU: an explicit host round trip between two graphs), "none" (no
+process group).  ``SAE_WORLD1_RCCL=1`` (bench.py ``--world1-rccl``) creates a world-size-1 RCCL
+group so the overlapped collective path runs on a one-GPU box.
 
 Loss: one-hot -> optax.smooth_labels(0.1) -> softmax cross-entropy, mean (train.py:83-92).
 Optimizer: Adam + decoupled weight decay 1e-4, lr 5e-4 * batch/512 (train.py:25-27,229-233;
@@ -39,7 +48,9 @@ def smoothed_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, smoothing
 
 
 def init_distributed():
-    """Initialise the process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    """Initialise the process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
+    ``SAE_WORLD1_RCCL=1`` at world size 1 (GPU): a one-rank RCCL group, so the training step's
+    collective path (the overlapped bucket all-reduces captured in the step's HIP graph) runs."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -48,13 +59,34 @@ def init_distributed():
     backend = os.environ.get("SAE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
-    if world > 1 and not dist.is_initialized():
+    world1 = world == 1 and os.environ.get("SAE_WORLD1_RCCL", "0") == "1" and torch.cuda.is_available()
+    if (world > 1 or world1) and not dist.is_initialized():
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        if world1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            dist.init_process_group(backend="nccl", rank=0, world_size=1)
+        else:
+            dist.init_process_group(backend=backend)
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
+
+
+def flat_layout(params, align: int = 4):
+    """Offsets of ``params`` in one flat fp32 buffer, each rounded up to ``align`` elements (16
+    bytes): every gradient view starts 16-byte aligned, as the vector stores of the kernels that
+    write them in place (gemm_dw, patch_embed_bwd, tokens_bwd) require.  Returns (offsets, total)."""
+    offs, off = [], 0
+    for p in params:
+        offs.append(off)
+        off += -(-p.numel() // align) * align
+    return offs, off
 
 
 class FusedAdamW:
@@ -107,20 +139,22 @@ class FusedAdamW:
 
 
 class TrainStep:
-    """``step(images, labels)`` = forward (bf16 compute) + loss + backward (+ bucketed RCCL
-    all-reduce of the flat gradient when world > 1) + optimizer update.  No host sync.
+    """``step(images, labels)`` = forward (bf16 compute) + loss + backward (+ bucketed all-reduce of
+    the flat gradient when there is a process group) + optimizer update.  No host sync.
 
-    graph=True (GPU): world == 1 -> the whole step is one HIP graph; world > 1 -> graph 1 =
-    forward + loss + backward, eager bucket all-reduces, graph 2 = AdamW."""
+    graph=True (GPU): the whole step is one HIP graph (collective "overlap" or "none"); with
+    ``two_graphs=True`` (collective "between") or the gloo rehearsal ("host"): graph 1 = forward +
+    loss + backward, the bucket all-reduces, graph 2 = AdamW."""
 
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
-                 label_smoothing: float = 0.1, bucket_cap_mb: float = 64.0, device: Optional[torch.device] = None,
+                 label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
                  graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None,
                  grad_sinks: bool = True, two_graphs: Optional[bool] = None):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.pg = dist.is_initialized()
+        self.world = dist.get_world_size() if self.pg else 1
         self.graph = bool(graph) and torch.cuda.is_available()
         self._g = self._g_opt = None
         self.model = model
@@ -128,39 +162,55 @@ class TrainStep:
         self._params = params
         if self.world > 1:
             self._broadcast_from_rank0([t for t in model.state_dict().values() if torch.is_tensor(t)])
-        # flat_grads (default: on the GPU, and whenever world > 1): one flat gradient buffer written
-        # in place by the backward kernels (gradient sinks), stepped by the one-launch FusedAdamW;
-        # two_graphs (default: world > 1): forward + backward and the optimizer as two graphs
-        # around the all-reduce (settable at world 1 to test that structure)
+        # flat_grads (default: on the GPU, and whenever there is a process group): one flat gradient
+        # buffer written in place by the backward kernels (gradient sinks), stepped by the one-launch
+        # FusedAdamW
         on_gpu = all(p.is_cuda for p in params)
-        self.flat = (self.world > 1 or on_gpu) if flat_grads is None else bool(flat_grads)
-        self.two_graphs = self.world > 1 if two_graphs is None else bool(two_graphs)
+        self.flat = (self.pg or on_gpu) if flat_grads is None else bool(flat_grads)
+        if not self.pg:
+            self.collective = "none"
+        elif on_gpu and dist.get_backend() == "gloo":
+            self.collective = "host"
+        elif two_graphs:
+            self.collective = "between"
+        else:
+            self.collective = "overlap"
+        if self.collective != "none" and not self.flat:
+            raise ValueError("TrainStep: the collective path needs the flat gradient buffer")
+        self.two_graphs = self.collective in ("between", "host") or (self.collective == "none" and bool(two_graphs))
         if self.flat:
-            # one flat fp32 gradient buffer, every .grad a view into it (autograd accumulates into
-            # the views in place), cut into buckets of ~bucket_cap_mb along parameter boundaries
-            # in reverse registration order (the order the backward finishes them)
-            n = sum(p.numel() for p in params)
+            # one flat fp32 gradient buffer, every .grad a 16-byte-aligned view into it (autograd
+            # accumulates into the views in place), cut into buckets of ~bucket_cap_mb along
+            # parameter boundaries in reverse registration order (the order the backward finishes
+            # them; a bucket closes once it holds >= cap elements)
+            offs, n = flat_layout(params)
+            self._offs = offs
             dev = params[0].device
             self._flat = torch.zeros(n, dtype=torch.float32, device=dev)
-            off = 0
-            for p in params:
+            for p, off in zip(params, offs):
                 p.grad = self._flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
             cap = max(1, int(bucket_cap_mb * 2 ** 20 / 4))
-            self._buckets, hi, lo = [], n, n
-            for p in reversed(params):
-                lo -= p.numel()
-                if hi - lo >= cap:   # close a bucket once it holds >= cap elements
+            self._buckets, self._bucket_params = [], []
+            hi, members = n, []
+            for i in reversed(range(len(params))):
+                members.append(i)
+                lo = offs[i]
+                if hi - lo >= cap:
                     self._buckets.append((lo, hi))
-                    hi = lo
-            if hi > 0:
+                    self._bucket_params.append(members)
+                    hi, members = lo, []
+            if members:
                 self._buckets.append((0, hi))
+                self._bucket_params.append(members)
+            self._bucket_of = {i: b for b, ms in enumerate(self._bucket_params) for i in ms}
             # the backward kernels write each parameter's gradient straight into its flat view
             # (ops.set_grad_sinks) instead of autograd adding a fresh gradient tensor into it
             self._sinks = bool(grad_sinks)
             if self._sinks:
                 from . import ops
                 ops.set_grad_sinks(params, [p.grad for p in params])
+            if self.collective == "overlap":
+                self._arm_overlap_hooks()
         base_lr = lr * (global_batch / 512)
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         self.opt = None
@@ -197,6 +247,68 @@ class TrainStep:
                     t.copy_(flat[off:off + t.numel()].view_as(t))
                     off += t.numel()
 
+    # ---- the overlapped bucket all-reduce
+    def _arm_overlap_hooks(self):
+        """A parameter's gradient is final when the kernel writing its sink has been enqueued
+        (ops.set_sink_listener) or, for gradients autograd accumulates, after its accumulation
+        (post-accumulate-grad hook); the bucket holding it is launched once all of its parameters
+        are final."""
+        from . import ops
+        self._armed = False
+        self._ptr_to_idx = {p.grad.data_ptr(): i for i, p in enumerate(self._params)}
+        ops.set_sink_listener(self._on_sink)
+        for i, p in enumerate(self._params):
+            p.register_post_accumulate_grad_hook(lambda _p, i=i: self._on_ready(i))
+        if self._flat.is_cuda:
+            self._comm = torch.cuda.Stream(device=self._flat.device)
+
+    def _on_sink(self, ptr):
+        i = self._ptr_to_idx.get(ptr)
+        if i is not None:
+            self._on_ready(i)
+
+    def _on_ready(self, i):
+        if not self._armed or i in self._ready:
+            return
+        self._ready.add(i)
+        b = self._bucket_of[i]
+        self._remaining[b] -= 1
+        if self._remaining[b] == 0:
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b):
+        lo, hi = self._buckets[b]
+        t = self._flat[lo:hi]
+        self._launched[b] = True
+        if t.is_cuda:
+            # the comm stream picks up everything enqueued so far on the compute stream (this
+            # bucket's gradient kernels included) and runs the RCCL all-reduce beside the rest of
+            # the backward; inside a graph capture this is a fork of the captured graph
+            self._comm.wait_stream(torch.cuda.current_stream(t.device))
+            with torch.cuda.stream(self._comm):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        else:
+            self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
+
+    def _begin_overlap(self):
+        self._ready = set()
+        self._remaining = [len(ms) for ms in self._bucket_params]
+        self._launched = [False] * len(self._buckets)
+        self._works = []
+        self._armed = True
+
+    def _end_overlap(self):
+        self._armed = False
+        for b in range(len(self._buckets)):   # buckets holding a parameter that got no gradient
+            if not self._launched[b]:
+                self._launch_bucket(b)
+        if self._flat.is_cuda:
+            torch.cuda.current_stream(self._flat.device).wait_stream(self._comm)   # the join
+        else:
+            for w in self._works:
+                w.wait()
+        self._works = []
+
     # ---- pieces of one step
     def _zero_grad(self):
         if self.flat:
@@ -215,47 +327,60 @@ class TrainStep:
         backward).  Graph mode only: the captured step writes the same sinks on every replay."""
         from . import ops
         written = set(ops._SINK_WRITTEN)
-        ranges, off = [], 0
-        for p in self._params:
+        ranges = []
+        for p, off in zip(self._params, self._offs):
             n = p.numel()
             if p.grad is None or p.grad.data_ptr() not in written:
                 if ranges and ranges[-1][1] == off:
                     ranges[-1] = (ranges[-1][0], off + n)
                 else:
                     ranges.append((off, off + n))
-            off += n
         # many scattered ranges would cost more launches than the one full fill saves
         self._zero_ranges = ranges if len(ranges) <= 8 else None
 
     def _fwd_bwd(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        from . import ops
         self._zero_grad()
-        if self.flat and self._sinks:
-            from . import ops
-            ops.begin_backward_sinks()
-        if self.input_layout == "NHWC":
-            logits = self.model(images, is_training=True)
-        else:
-            logits = self.model(images, is_training=True, layout=self.input_layout)
-        loss = smoothed_cross_entropy(logits, labels, self.smoothing)
-        # world > 1: the SUM all-reduce of the per-rank gradients of loss / world is the
-        # gradient of the global-batch mean (survey D9)
-        (loss / self.world if self.world > 1 else loss).backward()
-        if self.flat and self._sinks and self.graph and not torch.cuda.is_current_stream_capturing():
+        sinks = self.flat and self._sinks
+        overlap = self.collective == "overlap"
+        if sinks:
+            ops.begin_backward_sinks()   # the sink window: this step's forward + backward only
+        try:
+            if overlap:
+                self._begin_overlap()
+            if self.input_layout == "NHWC":
+                logits = self.model(images, is_training=True)
+            else:
+                logits = self.model(images, is_training=True, layout=self.input_layout)
+            loss = smoothed_cross_entropy(logits, labels, self.smoothing)
+            # world > 1: the SUM all-reduce of the per-rank gradients of loss / world is the
+            # gradient of the global-batch mean (survey D9)
+            (loss / self.world if self.world > 1 else loss).backward()
+            if overlap:
+                self._end_overlap()
+        finally:
+            if sinks:
+                ops.end_backward_sinks()
+            if overlap:
+                self._armed = False
+        if sinks and self.graph and not torch.cuda.is_current_stream_capturing():
             self._note_sunk()
         return loss.detach()
 
     def _allreduce(self):
-        if self.world == 1:
+        """The all-reduce between two graphs ("between" / "host"); "overlap" runs it inside the
+        backward and "none" has none."""
+        if self.collective in ("none", "overlap"):
             return
-        if self._flat.is_cuda and dist.get_backend() == "gloo":
+        if self.collective == "host":
             # rehearsal of the multi-rank step on fewer GPUs (SAE_DIST_BACKEND=gloo): one explicit
             # host round trip (gloo's own CUDA path stalled for seconds behind the graph replays)
             host = self._flat.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM)
             self._flat.copy_(host)
             return
-        # RCCL: every bucket in flight at once on the process group's stream; the optimizer's
-        # graph replay waits for them on the compute stream (no host synchronisation)
+        # every bucket in flight at once on the process group's stream; the optimizer's graph
+        # replay waits for them on the compute stream (no host synchronisation)
         works = [dist.all_reduce(self._flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True) for lo, hi in self._buckets]
         for w in works:
             w.wait()
@@ -278,7 +403,7 @@ class TrainStep:
                       for p in params if id(p) in had_state}
         s = torch.cuda.Stream(device=images.device)
         s.wait_stream(torch.cuda.current_stream(images.device))
-        with torch.cuda.stream(s):   # warm-up on a side stream (allocator / library state)
+        with torch.cuda.stream(s):   # warm-up on a side stream (allocator / library / communicator state)
             for _ in range(2):
                 self._eager(self._images, self._labels)
         torch.cuda.current_stream(images.device).wait_stream(s)
@@ -306,7 +431,7 @@ class TrainStep:
         if not self.flat:
             self.opt.zero_grad(set_to_none=True)
         try:
-            if not self.two_graphs:     # the whole step in one graph
+            if not self.two_graphs:     # the whole step (with the overlapped collectives) in one graph
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._loss = self._eager(self._images, self._labels)

@@ -60,3 +60,29 @@ def test_scaled_branch_equals_layerscale_then_stochdepth():
     b = sd(ls(x, torch.float32), True)
     assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
     assert torch.equal(cait.scaled_branch(x, ls, sd, torch.float32, False), ls(x, torch.float32))
+
+
+def test_cait_bf16_chain_tracks_fp64():
+    """The bf16-emulated oracle chain (the GPU bf16 checker) computes the same model as the fp64
+    oracle forward, up to bf16 rounding; with its rounding points removed it is the fp64 forward."""
+    import numpy as np
+    import torch
+    import cait_ref
+    from sae_vision_amd import cait
+    torch.manual_seed(0)
+    m = cait.CaiT(num_classes=10, num_layers=2, num_layers_token_only=2, num_heads=4, embed_dim=96,
+                  patch_shape=(16, 16), stoch_depth_rate=0.0, layerscale_eps=1.0, img_size=32, device="cpu")
+    with torch.no_grad():
+        m.Dense_0.kernel.normal_(0.0, 0.2)
+    P = {n: p.detach().double() for n, p in m.named_parameters()}
+    x = np.random.default_rng(0).standard_normal((2, 32, 32, 3))
+    ref = cait_ref.cait_forward({n: t.numpy() for n, t in P.items()}, x, 2, 2, 16)
+    got = cait_ref.cait_logits_bf16(P, x, 2, 2, 16).numpy()
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 3e-2
+    orig = cait_ref._torch_rb
+    try:
+        cait_ref._torch_rb = lambda: (lambda t: t)
+        exact = cait_ref.cait_logits_bf16(P, x, 2, 2, 16).numpy()
+    finally:
+        cait_ref._torch_rb = orig
+    assert np.abs(exact - ref).max() / np.abs(ref).max() < 1e-12

@@ -46,12 +46,22 @@ def _worker(rank, world, port, out):
     step = train.TrainStep(TinyNet(seed=rank), global_batch=x.shape[0], bucket_cap_mb=0.0001)
     # the flat gradient buffer: every .grad a view into it, buckets tile it from the end (the
     # order the backward completes the parameters), each at least the cap unless it is the last
-    n = sum(p.numel() for p in step.model.parameters())
+    # every view 16-byte aligned (the in-place gradient kernels' vector stores; l2.bias has 5 elements)
+    n = step._flat.numel()
     b = step._buckets
     assert b[0][1] == n and b[-1][0] == 0 and all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
     assert len(b) > 1 and all(p.grad.data_ptr() >= step._flat.data_ptr() for p in step.model.parameters())
+    assert all(p.grad.data_ptr() % 16 == 0 for p in step.model.parameters())
+    # the buckets' all-reduces are launched from inside the backward, as each bucket completes
+    assert step.collective == "overlap"
+    launched = []
+    orig = step._launch_bucket
+    step._launch_bucket = lambda bi: (launched.append((bi, len(step._ready))), orig(bi))[1]
     for _ in range(3):
         step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    # bucket 0 (the last parameters) goes out before the backward has finished every gradient
+    assert launched[0][0] == 0 and launched[0][1] < len(list(step.model.parameters())), launched
+    assert sorted(bi for bi, _ in launched[:len(b)]) == list(range(len(b)))
     flat = torch.cat([p.detach().flatten() for p in step.model.parameters()])
     gathered = [torch.zeros_like(flat) for _ in range(world)]
     dist.all_gather(gathered, flat)

@@ -72,10 +72,20 @@ def test_flat_grad_sinks_bitwise(dev, model):
         assert pa.grad is not None and pb.grad is not None, n
         assert pb.grad.data_ptr() >= s_b._flat.data_ptr(), n            # still the flat view
         assert torch.equal(pa.grad, pb.grad), (n, float((pa.grad - pb.grad).abs().max()))
-    # a second backward without begin_backward_sinks() re-claims the sinks: refused
-    with pytest.raises(RuntimeError, match="written twice"):
-        logits = m_b(x, is_training=True)
-        train.smoothed_cross_entropy(logits, y).backward()
+    # outside the training step's sink window a backward keeps autograd's accumulate semantics
+    g1 = [p.grad.clone() for p in m_b.parameters()]
+    train.smoothed_cross_entropy(m_b(x, is_training=True), y).backward()
+    torch.cuda.synchronize()
+    for (n, p), g in zip(m_b.named_parameters(), g1):
+        assert torch.allclose(p.grad, 2 * g, rtol=1e-5, atol=1e-6), n
+    # inside one window a parameter's sink can be written once: a second backward is refused
+    ops.begin_backward_sinks()
+    try:
+        train.smoothed_cross_entropy(m_b(x, is_training=True), y).backward()
+        with pytest.raises(RuntimeError, match="written twice"):
+            train.smoothed_cross_entropy(m_b(x, is_training=True), y).backward()
+    finally:
+        ops.end_backward_sinks()
     ops.set_grad_sinks(None)
 
 
@@ -127,8 +137,59 @@ def test_grad_sink_follows_param_grad(dev):
     for p in params:
         p.grad = None            # reset: the registered views are no longer the gradients
     ops.begin_backward_sinks()
-    x = torch.randn(2, 224, 224, 3, device=dev)
-    m(x, is_training=True).float().sum().backward()
+    try:
+        x = torch.randn(2, 224, 224, 3, device=dev)
+        m(x, is_training=True).float().sum().backward()
+    finally:
+        ops.end_backward_sinks()
     assert all(p.grad is not None for p in params)
     assert float(flat.abs().max()) == 0.0   # nothing went into the stale views
     ops.set_grad_sinks(None)
+
+
+@pytest.mark.parametrize("model", ["deit_ti_patch16", "cait"])
+def test_world1_rccl_overlapped_step(dev, model):
+    """The multi-rank step's collective path on one GPU: a one-rank RCCL group (backend nccl), the
+    bucket all-reduces launched from inside the backward on the communication stream and captured
+    with the rest of the step in ONE HIP graph (train.py "overlap").  A one-rank SUM is the
+    identity, so losses and parameters must equal the no-collective graph step's bit for bit; the
+    buckets must all have been launched, the first before the backward finished."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from sae_vision_amd import cait, train, vit
+    torch.manual_seed(0)
+    if model == "cait":
+        m_a = cait.create_cait("cait_xxs_24", 1000, torch.bfloat16, stoch_depth=False, device=dev)
+    else:
+        m_a = vit.create_model(model, 1000, torch.bfloat16, device=dev)
+    m_b = copy.deepcopy(m_a)
+    s_a = train.TrainStep(m_a, global_batch=8, device=dev, graph=True)
+    assert s_a.collective == "none"
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=True, bucket_cap_mb=4.0)
+        assert s_b.collective == "overlap" and len(s_b._buckets) > 1
+        order = []
+        orig = s_b._launch_bucket
+        s_b._launch_bucket = lambda bi: (order.append((bi, len(s_b._ready))), orig(bi))[1]
+        g = torch.Generator(device=dev).manual_seed(3)
+        data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
+                 torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
+        la = [float(s_a(x, y)) for x, y in data]
+        lb = [float(s_b(x, y)) for x, y in data]
+        assert s_b._g is not None and s_b._g_opt is None and s_b.graph   # one graph, collectives inside
+        nb = len(s_b._buckets)
+        assert sorted(bi for bi, _ in order[-nb:]) == list(range(nb))     # the captured backward's launches
+        assert order[-nb][1] < len(s_b._params)                            # the first before the last gradient
+        assert la == lb, (la, lb)
+        for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
+            assert torch.equal(pa, pb), n
+    finally:
+        dist.destroy_process_group()
+        from sae_vision_amd import ops
+        ops.set_sink_listener(None)

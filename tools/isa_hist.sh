@@ -1,7 +1,7 @@
 #!/bin/bash
 # Instruction histogram of one kernel (mangled-name substring) of the HIP library.
 cd "$(dirname "$0")/.." && mkdir -p /tmp/isa && cd /tmp/isa && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared \
-  -mllvm -amdgpu-mfma-vgpr-form=1 -fno-honor-nans -I /root/repo/include /root/repo/self-attention-experiments-vision_amd/csrc/capi.hip \
+  -mllvm -amdgpu-mfma-vgpr-form=1 -fno-honor-nans -fno-slp-vectorize -I /root/repo/include /root/repo/self-attention-experiments-vision_amd/csrc/capi.hip \
   -save-temps -o /tmp/isa/x.so 2>/dev/null
 python3 - "$1" <<'PY'
 import sys, re
