@@ -281,6 +281,11 @@ def main():
     args = ap.parse_args()
     if args.world1_rccl:
         os.environ["SAE_WORLD1_RCCL"] = "1"
+    # stdout carries exactly ONE line, the JSON result: everything else written to fd 1 by the
+    # libraries underneath (RCCL prints its version banner at communicator creation) goes to stderr
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -381,6 +386,7 @@ def main():
     if rank != 0:
         if world > 1:
             dist.barrier()
+        dist.destroy_process_group()
         return
     out = {
         "metric": METRIC, "value": round(img_s, 2), "unit": "img/s", "n_gpus": world, "steps": args.steps,
@@ -409,9 +415,11 @@ def main():
         out["attention_headline_f32"] = headline(dev, iters=5, reps=3, f32=True)
     if not args.profile and not args.no_cpu_baseline and world == 1 and args.img_size == 224 and not is_cait:
         out["cpu_baseline"] = cpu_baseline(args.model)
-    print(json.dumps(out), flush=True)
+    os.write(out_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -430,17 +430,21 @@ class TrainStep:
                         v.zero_()
         if not self.flat:
             self.opt.zero_grad(set_to_none=True)
+        # with a process group, RCCL's watchdog thread keeps querying the events of the warm-up's
+        # collectives while the capture runs: a "global" capture would refuse those queries
+        # (hipErrorStreamCaptureUnsupported, fatal in the watchdog), a thread-local one allows them
+        mode = "thread_local" if self.pg else "global"
         try:
             if not self.two_graphs:     # the whole step (with the overlapped collectives) in one graph
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=mode):
                     self._loss = self._eager(self._images, self._labels)
                 self._g = g
             else:                 # the collectives stay outside: two graphs around them
                 g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=mode):
                     self._loss = self._fwd_bwd(self._images, self._labels)
-                with torch.cuda.graph(go):
+                with torch.cuda.graph(go, capture_error_mode=mode):
                     self.opt.step()
                 self._g, self._g_opt = g, go
         except RuntimeError as e:   # an op that cannot be captured: stay eager, say so once
