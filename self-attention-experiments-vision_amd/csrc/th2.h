@@ -216,7 +216,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   char* ldsV = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
-  const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
+  // XCD-aware order: the query blocks of one image run on one XCD and share its K / V in L2
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = lb % nqb, b = lb / nqb;
   const int q = qb * 32 + r32;
   const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
@@ -402,7 +404,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   char* ldsK = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
-  const int qb = blockIdx.x % nqb, b = blockIdx.x / nqb;
+  // XCD-aware order: the query blocks of one image run on one XCD and share its K / V in L2
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = lb % nqb, b = lb / nqb;
   const int q = qb * 32 + r32;
   const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
@@ -602,7 +606,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   char* buf = MX + kTh2MixTbl + w * I::bytes(32);
 
   const int nkb = (a.Nk + 31) / 32;
-  const int kb = blockIdx.x % nkb, b = blockIdx.x / nkb;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);   // the key blocks of one image on one XCD
+  const int kb = lb % nkb, b = lb / nkb;
   const int key = kb * 32 + r32;
   const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
