@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Build libsae_attn.so in-tree for gfx950 (hipcc cross-compiles; no GPU needed).
 
-Usage: python build.py [--force] [--debug] [--dev]
+Usage: python build.py [--force] [--debug] [--dev] [--stamps]
 
 --dev builds the development library libsae_attn_dev.so (schedule-variant knobs read from the
-environment, SAE_DEV_KNOBS); tools load it through SAE_ATTN_LIB.  The release library
+environment, SAE_DEV_KNOBS); tools load it through SAE_ATTN_LIB.  --stamps builds
+libsae_attn_stamp.so (the dev knobs plus in-kernel s_memtime stamps, tools/stamps.py).  The release library
 libsae_attn.so never reads the environment on a launch path.
 """
 import argparse
@@ -17,6 +18,7 @@ PKG = os.path.join(ROOT, "self-attention-experiments-vision_amd")
 SRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "libsae_attn.so")
 OUT_DEV = os.path.join(PKG, "libsae_attn_dev.so")
+OUT_STAMP = os.path.join(PKG, "libsae_attn_stamp.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SAE_ARCH", "gfx950")
 
@@ -33,23 +35,45 @@ def up_to_date(out=OUT):
     return all(os.path.getmtime(p) <= t for p in deps)
 
 
-def build(force=False, debug=False, verbose=True, dev=False):
-    out = OUT_DEV if dev else OUT
+# translation units: (source, extra flags).  capi.hip keeps every MFMA accumulator in VGPRs
+# (-amdgpu-mfma-vgpr-form: the exp / rescale VALU reads them directly); bwd_agpr.hip holds the
+# one-wave-per-SIMD kernels, whose dK / dV accumulators go to the AGPR half of the register file.
+UNITS = [("capi.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd_agpr.hip", [])]
+
+
+def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
+    out = OUT_STAMP if stamps else (OUT_DEV if dev else OUT)
     if not force and up_to_date(out):
         if verbose:
             print(f"[build] {out} is up to date")
         return out
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"),
-           os.path.join(SRC, "capi.hip"), "-o", out + ".tmp"]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+              "-fno-honor-nans", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include")]
     if debug:
-        cmd.insert(3, "-g")
-    if dev:
-        cmd.insert(3, "-DSAE_DEV_KNOBS")
+        common.append("-g")
+    if dev or stamps:
+        common.append("-DSAE_DEV_KNOBS")
+    if stamps:
+        common.append("-DSAE_STAMPS")
+    tag = os.path.basename(out).replace(".so", "")
+    objs, procs = [], []
+    for src, extra in UNITS:
+        obj = os.path.join(PKG, f".{tag}.{src}.o")
+        cmd = common + extra + ["-c", os.path.join(SRC, src), "-o", obj]
+        if verbose:
+            print("[build]", " ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    for p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, "hipcc")
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
-        print("[build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        print("[build]", " ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
     return out
 
 
@@ -58,6 +82,7 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--dev", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic build with in-kernel cycle stamps")
     a = ap.parse_args()
-    build(a.force, a.debug, dev=a.dev)
+    build(a.force, a.debug, dev=a.dev, stamps=a.stamps)
     sys.exit(0)

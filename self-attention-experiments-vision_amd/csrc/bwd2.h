@@ -32,6 +32,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nqb = (a.Nq + BQ - 1) / BQ;
+  SAE_STAMPO(4096, 0);
   int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb;
   bid /= nqb;
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
   if constexpr (REL) rel_put_onehot<NW>(a, rimg, 0, tid);
   vm_wait_all();   // Q / dO fragments resident before the loop (see vm_wait_all)
   __syncthreads();
+  SAE_STAMPO(4096, 1);
   // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1, barrier (as fwd2.h)
   auto step = [&](int t, auto bsel_c, auto first_c, auto compute_c) {
     constexpr int bsel = decltype(bsel_c)::value;
@@ -217,6 +219,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       if constexpr (REL) rel_put_onehot<NW>(a, rimg + (bsel ^ 1) * kRelImg, 64 * (t + 1), tid);
     }
     __syncthreads();
+    SAE_STAMPO(4096, 2 + (t < 27 ? t : 27));
   };
   auto sweep = [&](auto compute_c) {
     using B0 = std::integral_constant<int, 0>;
@@ -239,12 +242,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
       }
     }
   }
+  SAE_STAMPO(4096, 30);
   if (active) {
     const int q0 = qb * BQ + w * 32;
     __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
     wave_store_rows<DP, ROT ? -1 : 0>(adq, a.scale, smem + w * 32 * DP * 2, DQ, a.dqs[1], a.Nq - q0, a.D, lane,
                                       &a.rope, q0);
   }
+  SAE_STAMPO(4096, 31);
 }
 
 // --------------------------------------------------------------------------- dK / dV pass
@@ -254,7 +259,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
 // dV^T += dO^T P and dK^T += Q^T dS (transposed reads of the dO / Q images).
 // REL: the staged tile also carries the query-bias rows of its 64 queries ([64][32] bf16 image),
 // the wave's keys hold their one-hot rows in registers.
-template <int DP, int NW, int MINW, bool ROT = false, bool REL = false>
+// PIPE: full 64-query tiles issue both halves' S / dP chains back to back so that the scheduler
+// can run one half's exponentials under the other half's MFMAs (needs the registers of a
+// one-wave-per-SIMD build: MINW = 1, accumulators in AGPRs -- the bwd_agpr.hip instances).
+template <int DP, int NW, int MINW, bool ROT = false, bool REL = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -264,6 +272,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nkb = (a.Nk + BK - 1) / BK;
+  SAE_STAMP(0);
   int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kb = bid % nkb;
   bid /= nkb;
@@ -376,6 +385,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   put(0, smem, 0);
   vm_wait_all();   // K / V fragments resident before the loop (see vm_wait_all)
   __syncthreads();
+  SAE_STAMP(1);
   auto step = [&](int qt, auto bsel_c, auto first_c, auto compute_c) {
     constexpr int bsel = decltype(bsel_c)::value;
     constexpr bool FIRST = decltype(first_c)::value;
@@ -385,7 +395,63 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     const float* ldsD = ldsL + 64;
     char* nxt = smem + (bsel ^ 1) * TB;
     if (qt + 2 < nqt) fetch(bsel, qt + 2);   // register set bsel went to LDS at the end of tile qt - 1
-    if constexpr (decltype(compute_c)::value) {
+    bool piped = false;
+    if constexpr (PIPE && !REL && decltype(compute_c)::value) {
+      if (qt * 64 + 32 < a.Nq) {   // both halves hold query rows
+        piped = true;
+        f32x16 sp[2], dp[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          bf16x8 dla;
+          const float nd = -ldsD[32 * u + r32];
+          const __bf16 hi = (__bf16)nd;
+          const __bf16 lo = (__bf16)(nd - (float)hi);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dla[j] = (__bf16)0.f;
+          if (h == 0) {
+            dla[0] = hi;
+            dla[1] = lo;
+          }
+          sp[u] = zero16();
+          dp[u] = MF<__bf16>::mma(dla, one01, zero16());
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
+            const bf16x8 gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+            sp[u] = MF<__bf16>::mma(qr, kf[s], sp[u]);
+            dp[u] = MF<__bf16>::mma(gr, vf[s], dp[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float p = ex2(__builtin_fmaf(sp[u][4 * g + j], sl2, -l4[j]));
+              sp[u][4 * g + j] = p;
+              dp[u][4 * g + j] *= p;
+            }
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 pf = acc_frag<__bf16>(sp[u], s2);
+            const bf16x8 sf = acc_frag<__bf16>(dp[u], s2);
+            const bool z = FIRST && u == 0 && s2 == 0;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+              const int ro = (32 * u + 16 * s2) * DP * 2;
+              const bf16x8 gv = tr2(ldsG + ca[2 * tt] + ro, ldsG + ca[2 * tt + 1] + ro);
+              adv[tt] = MF<__bf16>::mma(gv, pf, z ? zero16() : adv[tt]);
+              const bf16x8 qv = tr2(ldsQ + ca[2 * tt] + ro, ldsQ + ca[2 * tt + 1] + ro);
+              adk[tt] = MF<__bf16>::mma(qv, sf, z ? zero16() : adk[tt]);
+            }
+          }
+        }
+      }
+    }
+    if (!piped && decltype(compute_c)::value) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (u == 1 && qt * 64 + 32 >= a.Nq) break;
@@ -450,6 +516,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     }
     if (qt + 1 < nqt) put(bsel ^ 1, nxt, qt + 1);
     __syncthreads();
+    SAE_STAMP(2 + (qt < 27 ? qt : 27));
   };
   auto sweep = [&](auto compute_c) {
     using B0 = std::integral_constant<int, 0>;
@@ -462,6 +529,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   };
   if (active) sweep(std::true_type{});   // waves past the last key only stage and sync
   else sweep(std::false_type{});
+  SAE_STAMP(30);
   if (active) {
     const int k0 = kb * BK + w * 32;
     char* scr = smem + w * 32 * DP * 2;
@@ -471,6 +539,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     wave_store_rows<DP>(adv, 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
   }
   (void)key;
+  SAE_STAMP(31);
 }
 
 }  // namespace sae

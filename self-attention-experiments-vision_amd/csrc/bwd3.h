@@ -50,14 +50,6 @@ template <int DP, int NW, int KPW> struct B3 {
 // bank-conflict free.
 __device__ __forceinline__ int ds_off(int r, int s) { return r * 64 + 8 * (s ^ ((r >> 1) & 7)); }
 
-typedef __attribute__((ext_vector_type(8))) short s16x8;
-
-__device__ __forceinline__ bf16x8 tr2(const char* p1, const char* p2) {
-  const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
-  const s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
-  const s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 template <int CTRL> __device__ __forceinline__ float dpp_mov(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
@@ -135,6 +127,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const dsb = smem + 2 * TB;   // two dS^T images (the K image during the prologue)
 
+  SAE_STAMP(0);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int hh = bid % a.H;
   const int b = bid / a.H;
@@ -193,6 +186,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
   st.template write<ROT>(smem, tid, &a.rope);
   vm_wait_all();
   __syncthreads();
+  SAE_STAMP(1);
 
   // dQ^T tiles of this wave: head-dim block db (16 wide) x query halves qh (16 rows) of each tile
   const int db = w % C::NDB;
@@ -255,6 +249,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
   for (int j = 0; j < 8; ++j) one01[j] = (__bf16)((h == 0 && j < 2) ? 1.f : 0.f);
   const float sl2 = a.scale * kLog2e;
   __syncthreads();   // every wave holds its K^T fragments: the K image becomes the dS images
+  SAE_STAMP(2);
   if (!active) {     // a wave past the last key writes zero dS once (its K rows are zero)
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
     const bf16x4 z = {};
@@ -383,6 +378,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
     if (qt > 0) dq_tile(dsb + (bsel ^ 1) * C::DSIMG, qt - 1);
     if (qt + 1 < nqt) st.template write<ROT>(smem + (bsel ^ 1) * TB, tid, &a.rope);
     __syncthreads();
+    SAE_STAMP(3 + (qt < 26 ? qt : 26));
   };
   {
     using B0 = std::integral_constant<int, 0>;
@@ -394,6 +390,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
   }
   dq_tile(dsb + ((nqt - 1) & 1) * C::DSIMG, nqt - 1);
   __syncthreads();   // every image read: the LDS becomes the per-wave store scratch
+  SAE_STAMP(30);
   if (active) {
 #pragma unroll
     for (int j = 0; j < KPW; ++j) {
@@ -406,6 +403,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       wave_store_rows<DP>(adv[j], 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
     }
   }
+  SAE_STAMP(31);
 }
 
 }  // namespace sae

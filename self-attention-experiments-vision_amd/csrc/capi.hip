@@ -19,6 +19,7 @@
 #include "fwd2.h"
 #include "bwd2.h"
 #include "bwd3.h"
+#include "bwd3p.h"
 #include "cls.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
@@ -166,15 +167,16 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 };
 
 // lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false>
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false,
+          bool FIX = false>
 int fwd2_run(hipStream_t st, const AttnArgs& a) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   const long long grid = (long long)nqb * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
   const size_t lds = 4 * (size_t)F2<DP>::TILE + (REL ? 2 * kRelImg : 0);
-  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL>), dim3((unsigned)grid), dim3(64 * NW), lds,
-                     st, a);
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX>), dim3((unsigned)grid), dim3(64 * NW),
+                     lds, st, a);
   return check_launch("attn_fwd2");
 }
 
@@ -226,9 +228,19 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
     case 4: return fwd2_run<DP, 4, 2, true>(st, a);
     case 5: return fwd2_run<DP, 4, 3, true>(st, a);
     case 6: return fwd2_run<DP, 4, 3, false>(st, a);
+    case 7: return fwd2_run<DP, 4, 3, true, false, DP / 16, false, true>(st, a);
+    case 8: return fwd2_run<DP, 4, 2, true, false, DP / 16, false, true>(st, a);
+    case 9: return fwd2_run<DP, 4, 3, false, false, DP / 16, false, true>(st, a);
     default: break;
   }
 #endif
+  // D <= 64 without rotary: three waves per SIMD, row sum on the VALU, running max fixed by the
+  // first tile (FIX, with the tracking sweep as the in-kernel fallback): 23.2 vs 24.6 us at
+  // DeiT-S, 95.4 vs 96.5 us at ViT-B@384 (profiles/r03b_fwdvar.txt, bitwise-equal outputs)
+  if constexpr (DP <= 64 && !ROT) {
+    if (DP == 64 && a.D <= 48) return fwd2_run<DP, 4, 3, false, false, 3, false, true>(st, a);
+    return fwd2_run<DP, 4, 3, false, false, DP / 16, false, true>(st, a);
+  }
   // long key ranges at D <= 64: three waves per SIMD, row sum on the VALU is 2.5 % faster at
   // N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt); at
   // D = 128 it is 2x slower
@@ -266,6 +278,26 @@ template <int DP, bool ROT = false> int bwd2_run_default(hipStream_t st, const A
   return bwd2_run<DP, 4, 2, 4, 2, ROT>(st, a);
 }
 
+}  // namespace
+namespace sae {
+hipError_t bwd2_dkdv_agpr(hipStream_t st, const AttnArgs& a, int dp, bool pipe);   // bwd_agpr.hip
+}
+namespace {
+
+// two-pass backward with the dK / dV pass from bwd_agpr.hip (one wave per SIMD, AGPR accumulators)
+template <int DP> int bwd2_run_agpr(hipStream_t st, const AttnArgs& a, bool pipe) {
+  {
+    const long long grid = (long long)((a.Nq + 127) / 128) * a.H * a.B;
+    if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+    const size_t lds = 4 * (size_t)F2<DP>::TILE;
+    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, 4, 2>), dim3((unsigned)grid), dim3(256), lds, st, a);
+    if (int rc = check_launch("attn_bwd2_dq")) return rc;
+  }
+  const hipError_t e = bwd2_dkdv_agpr(st, a, DP, pipe);
+  if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd2_dkdv (agpr): %s", hipGetErrorString(e));
+  return ok();
+}
+
 // single-pass bf16 backward (bwd3.h): one workgroup per (batch, head) holding all Nk <= 256 keys
 // (8 waves x 32 keys, two waves per SIMD); longer key ranges take the two-pass bwd2
 constexpr int kB3Keys = 256;
@@ -279,6 +311,28 @@ template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16> int bwd3
   if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>, C::LDS)) return rc;
   hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
   return check_launch("attn_bwd3");
+}
+
+// persistent single-pass backward (bwd3p.h): one workgroup per CU walking the (batch, head) units
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+  }
+  return n;
+}
+template <int DP, int NSU = DP / 16> int bwd3p_run(hipStream_t st, const AttnArgs& a) {
+  using C = B3<DP, 8, 1>;
+  using P = B3P<DP, 8>;
+  if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3p: %d keys > %d", a.Nk, C::BK);
+  const long long units = (long long)a.H * a.B;
+  if (units > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
+  const int grid = (int)std::min<long long>(units, num_cus());
+  if (int rc = lds_attr((const void*)attn_bwd3p_kernel<DP, 8, NSU>, P::LDS)) return rc;
+  hipLaunchKernelGGL((attn_bwd3p_kernel<DP, 8, NSU>), dim3((unsigned)grid), dim3(512), P::LDS, st, a);
+  return check_launch("attn_bwd3p");
 }
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
@@ -680,8 +734,13 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && !rel) {
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;
-    if (a.Nk <= kB3Keys && var != 2 && dp <= 64) {
+    if (a.Nk <= kB3Keys && var != 2 && var < 10 && dp <= 64) {
 #ifdef SAE_DEV_KNOBS
+      if (var == 20) {   // persistent bwd3 with the next unit's K / V prefetched by LDS-DMA
+        if (dp == 32) return bwd3p_run<32>(st, a);
+        if (dp == 64 && d->head_dim <= 48) return bwd3p_run<64, 3>(st, a);
+        if (dp == 64) return bwd3p_run<64>(st, a);
+      }
       if (var == 3) {   // four waves x two 32-key sub-blocks (one wave per SIMD): measured slower
         if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
         if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
@@ -691,6 +750,9 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
       if (dp == 64 && d->head_dim <= 48) return bwd3_run<64, 8, 1, false, 3>(st, a);   // CaiT head_dim 48
       if (dp == 64) return bwd3_run<64, 8, 1>(st, a);
     }
+#ifdef SAE_DEV_KNOBS
+    if (dp == 64 && (var == 10 || var == 11)) return bwd2_run_agpr<64>(st, a, var == 11);
+#endif
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);
     // head_dim 128 (BoTNet): one wave per SIMD (the dK / dV accumulators of 32 keys x 128 columns
@@ -1513,5 +1575,22 @@ const char* sae_last_error(void) { return g_err.c_str(); }
 int32_t sae_abi_version(void) { return SAE_ABI_VERSION; }
 
 const char* sae_build_info(void) { return "sae_attn gfx950 (" __DATE__ " " __TIME__ ")"; }
+
+#ifdef SAE_STAMPS
+// diagnostic build only (not declared in sae_attn.h): copy / clear the in-kernel stamp table
+int sae_dev_stamps(void* dst, size_t bytes, int clear) {
+  if (bytes > sizeof(unsigned long long) * (size_t)kStampRecs) return fail(SAE_EINVAL, "stamps: %zu bytes", bytes);
+  hipError_t e;
+  if (clear) {
+    void* p = nullptr;
+    e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_sae_stamps));
+    if (e == hipSuccess) e = hipMemset(p, 0, sizeof(unsigned long long) * (size_t)kStampRecs);
+  } else {
+    e = hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_sae_stamps), bytes, 0, hipMemcpyDeviceToHost);
+  }
+  if (e != hipSuccess) return fail(SAE_EHIP, "stamps: %s", hipGetErrorString(e));
+  return ok();
+}
+#endif
 
 }  // extern "C"

@@ -56,6 +56,32 @@ template <> struct MF<float> {
 
 __device__ __forceinline__ f32x16 zero16() { return f32x16{}; }
 
+// In-kernel cycle stamps (diagnostic build only: build.py --stamps defines SAE_STAMPS; the
+// release library compiles SAE_STAMP to nothing).  Lane 0 of every wave records the shader clock
+// (s_memtime) at slot `slot` of its (block, wave) record with a plain vector store; the host reads
+// the table back through sae_dev_stamps (capi.hip).  cdna_hip_programming.md §7 "In-kernel stamps".
+#ifdef SAE_STAMPS
+constexpr int kStampSlots = 32, kStampWaves = 16, kStampRecs = 1 << 22;
+__device__ unsigned long long g_sae_stamps[kStampRecs];
+// slot 0 (entry) and 31 (exit) also record the 100 MHz real-time clock in slots 28 / 29
+#define SAE_STAMPO(boff, slot)                                                                       \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0) {                                                                   \
+      const size_t i_ = ((size_t)(blockIdx.x + (boff)) * kStampWaves + (threadIdx.x >> 6)) * kStampSlots; \
+      if (i_ + kStampSlots <= (size_t)kStampRecs) {                                                   \
+        g_sae_stamps[i_ + (slot)] = __builtin_amdgcn_s_memtime();                                    \
+        if ((slot) == 0) g_sae_stamps[i_ + 28] = __builtin_amdgcn_s_memrealtime();                   \
+        if ((slot) == 31) g_sae_stamps[i_ + 29] = __builtin_amdgcn_s_memrealtime();                  \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
+#else
+#define SAE_STAMPO(boff, slot) \
+  do {                         \
+  } while (0)
+#endif
+#define SAE_STAMP(slot) SAE_STAMPO(0, slot)
+
 // s_waitcnt vmcnt(0) as a real S_WAITCNT (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait).  Put it
 // after prologue loads whose registers stay live through a loop: otherwise the waitcnt pass,
 // seeing them possibly outstanding at the loop header, waits at their first use INSIDE the loop
@@ -112,6 +138,16 @@ template <typename T, int DP> struct Img {
     }
   }
 };
+
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+// two ds_read_b64_tr_b16 (4 x 16 blocks at p1 and p2) as one 8-element bf16 MFMA operand
+__device__ __forceinline__ bf16x8 tr2(const char* p1, const char* p2) {
+  const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+  const s16x4 x2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p2));
+  const s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 // accumulator registers KH*s .. KH*s+KH-1 as an operand fragment
 template <typename T> __device__ __forceinline__ typename MF<T>::frag acc_frag(const f32x16& acc, int s) {

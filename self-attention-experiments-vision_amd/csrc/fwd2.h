@@ -134,7 +134,12 @@ struct F2Stage {
 // NSU: the 16-wide k-steps of QK^T that carry head-dim columns (3 for D = 48 at DP = 64: the
 // fourth would multiply zero padding)
 // REL: ldsR = the tile's one-hot image, ra = this lane's row reads of it, qa = query-bias rows
-template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS, bool REL = false>
+// FIX: the running max stays where the first tile put it (no per-tile row max, no rescale); the
+// kernel checks the row sums after the sweep and redoes the block with the tracking sweep if any
+// row's sum left [1, 2^64) (a later tile's score more than 64 log2 units above the first tile's
+// max).  P is fed to the MFMA in bf16, whose relative precision does not depend on magnitude,
+// so the result is that of the tracking sweep up to fp32 summation order.
+template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS, bool REL = false, bool FIX = false>
 __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
                                           f32x16& lacc, float& m, float& l, int nvalid, float sl2,
                                           const unsigned* ka, const unsigned* va, int h,
@@ -174,6 +179,7 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
       s1[r] = c + 32 < nvh ? s1[r] : -kInf;
     }
   }
+  if constexpr (FIRST || !FIX) {
   float mx = s0[0];
 #pragma unroll
   for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s0[r]);
@@ -198,6 +204,7 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
     } else {
       l *= alpha;
     }
+  }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) s0[r] = ex2(__builtin_fmaf(s0[r], sl2, -m));
@@ -257,13 +264,15 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 // K tile as it goes to LDS -- so the rotated tensors never exist in HBM.
 // REL: BoTNet relative logits as two extra score k-steps (rel_onehot8 / rel_qrow8 above); the
 // one-hot images follow the K / V buffers in LDS.
-template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false>
+template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false,
+          bool FIX = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = NSU, NT = FF::NT, TILE = FF::TILE;
   constexpr int BQ = 32 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+  SAE_STAMP(0);
   const int nqb = (a.Nq + BQ - 1) / BQ;
   int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb;
@@ -343,10 +352,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   if constexpr (REL) rel_put_onehot<NW>(a, rimg, 0, tid);
   vm_wait_all();   // Q fragments resident before the loop (see vm_wait_all)
   __syncthreads();
+  SAE_STAMP(1);
   // one K/V tile: load t + 1, compute t from LDS buffer BSEL, stage t + 1 into the other
   // buffer, barrier.  Buffer selection and the peeled first tile are compile-time, so the
   // first tile's zero accumulators become the MFMA's C operand and its rescale disappears.
-  auto step = [&](int t, auto bsel_c, auto first_c, auto compute_c) {
+  auto step = [&](int t, auto bsel_c, auto first_c, auto compute_c, auto fix_c) {
     constexpr int bsel = decltype(bsel_c)::value;
     char* cur = smem + bsel * 2 * TILE;
     char* nxt = smem + (bsel ^ 1) * 2 * TILE;
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       vst.load(rv, (unsigned)(t + 1) * vstep);
     }
     if constexpr (decltype(compute_c)::value)
-      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU, REL>(cur, cur + TILE, qf, acco, lacc, m, l,
+      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU, REL, decltype(fix_c)::value>(cur, cur + TILE, qf, acco, lacc, m, l,
                                                              min(64, a.Nk - 64 * t), sl2, ka, va, h,
                                                              rimg + bsel * kRelImg, ra, qa);
     if (t + 1 < nkt) {
@@ -365,20 +375,37 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       if constexpr (REL) rel_put_onehot<NW>(a, rimg + (bsel ^ 1) * kRelImg, 64 * (t + 1), tid);
     }
     __syncthreads();
+    SAE_STAMP(2 + (t < 27 ? t : 27));
   };
-  auto sweep = [&](auto compute_c) {
+  auto sweep = [&](auto compute_c, auto fix_c) {
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-    step(0, B0{}, std::true_type{}, compute_c);
+    step(0, B0{}, std::true_type{}, compute_c, fix_c);
     for (int t = 1; t < nkt; t += 2) {
-      step(t, B1{}, std::false_type{}, compute_c);
-      if (t + 1 < nkt) step(t + 1, B0{}, std::false_type{}, compute_c);
+      step(t, B1{}, std::false_type{}, compute_c, fix_c);
+      if (t + 1 < nkt) step(t + 1, B0{}, std::false_type{}, compute_c, fix_c);
     }
   };
   // waves past the last query row only stage tiles and meet the barriers
-  if (active) sweep(std::true_type{});
-  else sweep(std::false_type{});
+  if (active) sweep(std::true_type{}, std::bool_constant<FIX>{});
+  else sweep(std::false_type{}, std::bool_constant<FIX>{});
+  if constexpr (FIX) {   // a row whose sum left [1, 2^64): redo the block with the tracking sweep
+    const float lt0 = LSUM ? lacc[0] : xhalf_sum(l);
+    if (__syncthreads_or(active && q < a.Nq && !(lt0 < 0x1p64f))) {
+      kst.load(rk, 0);
+      vst.load(rv, 0);
+      if constexpr (ROT) kst.rope(a.rope, 0, tid);
+      kst.write(smem);
+      vst.write(smem + TILE);
+      if constexpr (REL) rel_put_onehot<NW>(a, rimg, 0, tid);
+      vm_wait_all();
+      __syncthreads();
+      if (active) sweep(std::true_type{}, std::false_type{});
+      else sweep(std::false_type{}, std::false_type{});
+    }
+  }
 
+  SAE_STAMP(30);
   if (!active) return;
   float lt;
   if constexpr (LSUM) lt = lacc[0];
@@ -394,6 +421,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
     wave_store_rows<DP>(acco, 1.f, smem + w * 32 * DP * 2, O, a.os[1], a.Nq - q0, a.D, lane);
   }
   if (q < a.Nq && h == 0 && a.lse) a.lse[((size_t)b * a.H + hh) * a.Nq + q] = (m + lg2(lt)) * kLn2;
+  SAE_STAMP(31);
 }
 
 }  // namespace sae

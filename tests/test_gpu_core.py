@@ -130,8 +130,8 @@ def test_deterministic(dev, N):
 @pytest.mark.parametrize("gain", [0.05, 0.6, 4.0])
 def test_softmax_spike(dev, mode, gain):
     """Forces the online-softmax max to jump at a late key tile (rule 26): gain 4 jumps far past
-    the lazy-rescale threshold (rescale branch), gain 0.6 jumps by a few log2 units (bf16: kept
-    below the threshold, P > 1 path), gain 0.05 barely moves it."""
+    the lazy-rescale threshold (rescale branch; ~46 log2 units, inside the bf16 forward's
+    fixed-max range), gain 0.6 jumps by a few log2 units (P > 1 path), gain 0.05 barely moves it."""
     import torch
     import sae_vision_amd.ops as ops
 
@@ -154,6 +154,33 @@ def test_softmax_spike(dev, mode, gain):
     g = R.attention_core_bwd(q, k, v, do)
     for n, t in (("dq", tq), ("dk", tk), ("dv", tv)):
         assert rel_err(t.grad, g[n]) <= TOL[mode], n
+
+
+@pytest.mark.parametrize("spike", [6, 12])
+def test_fixed_max_fallback(dev, spike):
+    """The bf16 forward keeps the running max where the first key tile put it and redoes a block
+    with the tracking sweep when a row sum leaves [1, 2^64) (fwd2.h FIX).  Integer-valued q / k
+    make every score exact in bf16 and fp32 (multiples of 1/8 below 128), so the oracle's
+    bf16-rounded scores equal the kernel's: spike 12 puts late scores ~93 log2 units above the
+    first tile's max (fallback taken), spike 6 up to ~55 units (fixed-max sweep kept)."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(11)
+    B, N, H, D = 2, 300, 2, 64
+    q = rng.integers(-1, 2, (B, N, H, D)).astype(np.float32)
+    k = rng.integers(-1, 2, (B, N, H, D)).astype(np.float32)
+    v = R.round_bf16(rng.standard_normal((B, N, H, D)).astype(np.float32))
+    for qi in (3, 40, 127, 200, 299):
+        k[:, 250 - qi // 3] = q[:, qi] * spike    # spike in a late tile
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=torch.bfloat16, requires_grad=True) for x in (q, k, v))
+    o = ops.attention(tq, tk, tv)
+    assert rel_err(o, R.attention_core_fwd(q, k, v, "bf16")) <= TOL["bf16"]
+    do = randn(np.random.default_rng(2), (B, N, H, D), "bf16")
+    o.backward(torch.tensor(do, device=dev, dtype=torch.bfloat16))
+    g = R.attention_core_bwd(q, k, v, do)
+    for n, t in (("dq", tq), ("dk", tk), ("dv", tv)):
+        assert rel_err(t.grad, g[n]) <= TOL["bf16"], n
 
 
 def test_error_reporting(dev):
