@@ -304,10 +304,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
   auto fetch = [&](int r, int qt) {
     qst[r].load(rq, (unsigned)qt * qstep);
     gst[r].load(rg, (unsigned)qt * gstep);
+    // raw values only: scaling or selecting them here would make the compiler wait for these
+    // loads (and, vmcnt counting in order, for the Q / dO loads above) right after issue, which
+    // drained the two-tile register prefetch every step; put() scales and masks them
     if (tid < 64) {
-      const int qq = qt * 64 + tid;
-      rc_l[r] = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
-      rc_d[r] = qq < a.Nq ? a.delta[rowoff + qq] : 0.f;
+      const int qq = min(qt * 64 + tid, a.Nq - 1);
+      rc_l[r] = a.lse[rowoff + qq];
+      rc_d[r] = a.delta[rowoff + qq];
     }
     if constexpr (REL) {
       static_assert(NW == 4, "REL staging: one query-bias chunk per thread");
@@ -374,8 +377,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dkdv_kernel(AttnArgs 
     qst[r].write(buf);
     gst[r].write(buf + TILE);
     if (tid < 64) {
-      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = rc_l[r];
-      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = rc_d[r];
+      const bool ok = qt * 64 + tid < a.Nq;
+      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = ok ? rc_l[r] * kLog2e : kInf;
+      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = ok ? rc_d[r] : 0.f;
     }
     if constexpr (REL) {
       const int rr = tid >> 2, c = tid & 3;

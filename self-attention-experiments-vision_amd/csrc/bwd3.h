@@ -64,8 +64,9 @@ template <int DP, int NW> struct B3Stage {
   int row, col;
   bool has;
   uint4 q, g, o;
-  float lse2;
+  float lse2;            // raw lse of row qt_ * 32 + tid (tid < 32), scaled by log2 e in write()
   int qt_;               // query tile held in the registers (rotary position base)
+  int nq_;
 
   __device__ __forceinline__ void init(int tid, const AttnArgs& a) {
     row = tid / C::CPR;
@@ -81,16 +82,17 @@ template <int DP, int NW> struct B3Stage {
                                        __amdgpu_buffer_rsrc_t ro, const AttnArgs& a, int qt, size_t rowoff,
                                        int tid) {
     qt_ = qt;
+    nq_ = a.Nq;
     q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                       rq, oq + (unsigned)(qt * 32 * a.qs[1] * 2), 0, 0));
     g = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                       rg, og + (unsigned)(qt * 32 * a.dos[1] * 2), 0, 0));
     o = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                       ro, oo + (unsigned)(qt * 32 * a.os[1] * 2), 0, 0));
-    if (tid < 32) {
-      const int qq = qt * 32 + tid;
-      lse2 = qq < a.Nq ? a.lse[rowoff + qq] * kLog2e : kInf;
-    }
+    // the raw lse only: scaling or selecting it here would make the compiler wait for this load --
+    // and with it for the q / dO / O loads above (vmcnt counts in order) -- right after issue,
+    // turning the register prefetch into a synchronous load at the top of every tile
+    if (tid < 32) lse2 = a.lse[rowoff + min(qt * 32 + tid, a.Nq - 1)];
   }
   template <bool ROT = false>
   __device__ __forceinline__ void write(char* buf, int tid, const RopeTab* rope = nullptr) const {
@@ -110,7 +112,7 @@ template <int DP, int NW> struct B3Stage {
       *reinterpret_cast<uint4*>(buf + C::QIMG + loff) = g;
       if (col == 0) reinterpret_cast<float*>(buf + 2 * C::QIMG + 128)[row] = -part;
     }
-    if (tid < 32) reinterpret_cast<float*>(buf + 2 * C::QIMG)[tid] = lse2;
+    if (tid < 32) reinterpret_cast<float*>(buf + 2 * C::QIMG)[tid] = qt_ * 32 + tid < nq_ ? lse2 * kLog2e : kInf;
   }
 };
 
