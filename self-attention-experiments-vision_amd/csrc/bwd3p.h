@@ -34,20 +34,55 @@ template <int DP, int NW> struct B3P {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
+// One 16-byte-per-lane LDS-DMA piece (1 KiB at the wave-uniform LDS byte address `lds`).  Inline
+// asm on purpose: issued through the builtin, the LDS-DMA makes hipcc put an s_waitcnt vmcnt(0)
+// in front of the first LDS read of every later tile (it cannot tell that the DMA's image is not
+// the one read), which drained the register prefetch of the next Q / dO tile in every iteration
+// (measured: 70 vs 55 us at DeiT-S).  Counted by hand instead: the unit's last wait (vm_wait_all +
+// barrier) retires it before any read of the image.  M0 is compiler-reserved: saved and restored
+// inside the statement (cdna_hip_programming.md §5.7: s_nop 4 for a fresh descriptor, s_nop 0
+// after the M0 write).
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+__device__ __forceinline__ void dma16(u32x4 rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds)
+      : "memory");
+}
+
+// the four words of row_rsrc's descriptor (common.h), for the inline-asm DMA
+template <typename T>
+__device__ __forceinline__ u32x4 row_rsrc_words(const T* base, int nrows, long long rs) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  u32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((unsigned)p);
+  r[1] = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32)) & 0xffffu;   // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((unsigned)((long long)nrows * rs * sizeof(T)));
+  r[3] = 0x00020000u;
+  return r;
+}
+
 // rows past Nk and columns past D read as zero through the buffer descriptor's range check
 template <int DP, int NW>
-__device__ __forceinline__ void b3p_dma_image(__amdgpu_buffer_rsrc_t rs, long long rowstride, int D, char* img,
-                                              int w, int lane) {
+__device__ __forceinline__ void b3p_dma_image(u32x4 rsw, long long rowstride, int D, char* img, int w, int lane) {
   using P = B3P<DP, NW>;
   constexpr int CPR = DP / 8;
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)img));
 #pragma unroll
   for (int i = 0; i < P::PIECES / NW; ++i) {
     const int piece = i * NW + w;
     const int r = piece * P::RPI + lane / CPR;
     const int c = (lane % CPR) ^ swz<DP>(r);   // the chunk this lane's 16 LDS bytes hold
     const unsigned off = (c * 8 < D) ? (unsigned)(((long long)r * rowstride + c * 8) * 2) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + piece * 1024), 16,
-                                             off, 0, 0, 0);
+    dma16(rsw, off, base + (unsigned)(piece * 1024));
   }
 }
 
@@ -99,12 +134,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd3p_kernel(AttnArgs a) {
   auto rsk = [&](int uu) {
     KArgs& a = arg();
     const int b = uu / a.H, hh = uu - b * a.H;
-    return row_rsrc(reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2], a.Nk, a.ks[1]);
+    return row_rsrc_words(reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2], a.Nk, a.ks[1]);
   };
   auto rsv = [&](int uu) {
     KArgs& a = arg();
     const int b = uu / a.H, hh = uu - b * a.H;
-    return row_rsrc(reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2], a.Nk, a.vs[1]);
+    return row_rsrc_words(reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2], a.Nk, a.vs[1]);
   };
   auto stage = [&](B3Stage<DP, NW>& st_, int uu, int qt) {
     st_.load(rsq(uu), rsg(uu), rso(uu), a, qt, (size_t)uu * a.Nq, tid);   // rowoff = (b H + hh) Nq

@@ -28,4 +28,36 @@ hipError_t bwd2_dkdv_agpr(hipStream_t st, const AttnArgs& a, int dp, bool pipe) 
   return hipErrorInvalidValue;
 }
 
+// both passes of the two-pass backward (bwd2.h) with the accumulators in AGPRs: dQ pass at MQ waves
+// per SIMD, dK / dV pass at MK (the head_dim 128 instances: BoTNet)
+template <int DP, int MQ, int MK, bool REL>
+hipError_t bwd2_agpr_launch(hipStream_t st, const AttnArgs& a) {
+  {
+    const long long grid = (long long)((a.Nq + 127) / 128) * a.H * a.B;
+    const size_t lds = 4 * (size_t)F2<DP>::TILE + (REL ? 2 * kRelImg : 0);
+    const void* fn = (const void*)attn_bwd2_dq_kernel<DP, 4, MQ, false, REL>;
+    if (lds > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, 4, MQ, false, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const long long grid = (long long)((a.Nk + 127) / 128) * a.H * a.B;
+  const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512 + (REL ? kRelImg : 0));
+  const void* fn = (const void*)attn_bwd2_dkdv_kernel<DP, 4, MK, false, REL>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, 4, MK, false, REL>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t bwd2_agpr128(hipStream_t st, const AttnArgs& a, bool rel, int variant) {
+  if (variant == 0) return rel ? bwd2_agpr_launch<128, 1, 1, true>(st, a) : bwd2_agpr_launch<128, 1, 1, false>(st, a);
+  return rel ? bwd2_agpr_launch<128, 2, 1, true>(st, a) : bwd2_agpr_launch<128, 2, 1, false>(st, a);
+}
+
 }  // namespace sae

@@ -237,9 +237,11 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
   // D <= 64 without rotary: three waves per SIMD, row sum on the VALU, running max fixed by the
   // first tile (FIX, with the tracking sweep as the in-kernel fallback): 23.2 vs 24.6 us at
   // DeiT-S, 95.4 vs 96.5 us at ViT-B@384 (profiles/r03b_fwdvar.txt, bitwise-equal outputs)
-  if constexpr (DP <= 64 && !ROT) {
-    if (DP == 64 && a.D <= 48) return fwd2_run<DP, 4, 3, false, false, 3, false, true>(st, a);
-    return fwd2_run<DP, 4, 3, false, false, DP / 16, false, true>(st, a);
+  // (the rotary instances take the same variant: the fused-rotary forward stays bit-equal to the
+  // standalone rotary pass + this forward, tests/test_gpu_rotary.py)
+  if constexpr (DP <= 64) {
+    if (!ROT && DP == 64 && a.D <= 48) return fwd2_run<DP, 4, 3, false, false, 3, false, true>(st, a);
+    return fwd2_run<DP, 4, 3, false, ROT, DP / 16, false, true>(st, a);
   }
   // long key ranges at D <= 64: three waves per SIMD, row sum on the VALU is 2.5 % faster at
   // N = 577 and equal at N = 197 (profiles/r01_attn_fwd_f0_vs_f6_interleaved_v13.txt); at
@@ -281,6 +283,7 @@ template <int DP, bool ROT = false> int bwd2_run_default(hipStream_t st, const A
 }  // namespace
 namespace sae {
 hipError_t bwd2_dkdv_agpr(hipStream_t st, const AttnArgs& a, int dp, bool pipe);   // bwd_agpr.hip
+hipError_t bwd2_agpr128(hipStream_t st, const AttnArgs& a, bool rel, int variant);  // bwd_agpr.hip
 }
 namespace {
 
@@ -755,6 +758,12 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
 #endif
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);
+#ifdef SAE_DEV_KNOBS
+    if (var == 30 || var == 31) {
+      const hipError_t e = bwd2_agpr128(st, a, false, var - 30);
+      return e == hipSuccess ? ok() : fail(SAE_EHIP, "bwd2 agpr: %s", hipGetErrorString(e));
+    }
+#endif
     // head_dim 128 (BoTNet): one wave per SIMD (the dK / dV accumulators of 32 keys x 128 columns
     // plus the K / V fragments need more than half the register file)
     return bwd2_run<128, 4, 1, 4, 1>(st, a);
@@ -764,6 +773,12 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     hipStream_t st = (hipStream_t)stream;
     if (dp == 32) return bwd2_run<32, 4, 2, 4, 2, false, true>(st, a);
     if (dp == 64) return bwd2_run<64, 4, 2, 4, 1, false, true>(st, a);
+#ifdef SAE_DEV_KNOBS
+    if (var == 30 || var == 31) {
+      const hipError_t e = bwd2_agpr128(st, a, true, var - 30);
+      return e == hipSuccess ? ok() : fail(SAE_EHIP, "bwd2 agpr: %s", hipGetErrorString(e));
+    }
+#endif
     return bwd2_run<128, 4, 2, 4, 1, false, true>(st, a);
   }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);

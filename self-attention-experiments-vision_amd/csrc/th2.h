@@ -169,6 +169,15 @@ __device__ __forceinline__ bf16x8 th2_colB(const char* img, int head, int s, int
   return th2_tr2(base + r1 * kTh2Blk, base + (r1 + 8) * kTh2Blk);
 }
 
+// operand fragment of row `row` (head-dim columns 16 s + 8 h .. + 7) through a buffer descriptor
+// over the valid rows (row_rsrc): rows past the end and columns >= D read as zero.  (gfrag's
+// branch-per-load form made hipcc wait vmcnt(0) after every fragment load: no prefetch survived.)
+__device__ __forceinline__ bf16x8 th2_frag(__amdgpu_buffer_rsrc_t rsrc, int row, long long rs, int D, int s, int h) {
+  const int d0 = 16 * s + 8 * h;
+  const unsigned off = d0 < D ? (unsigned)(((long long)row * rs + d0) * 2) : 0x80000000u;
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+}
+
 // th2_rowB: image row `head` read as a [column = lane][row] matrix (position = column * 32 + row:
 // the key-block kernel, B[k = query][column = key]): two 8-byte reads of query runs
 __device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int lane) {
@@ -223,6 +232,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
+  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
+                               rV = row_rsrc(V, a.Nk, a.vs[1]);
 
   th2_zero_pad<KST>(XS, H, tid, 64 * H);
   th2_zero_pad<KST>(XP, H, tid, 64 * H);
@@ -231,7 +242,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   bf16x8 qf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    qf[s] = th2_frag(rQ, q, a.qs[1], a.D, s, h);
     if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
   }
   const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);   // S1 = T1^T S
@@ -251,7 +262,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   bf16x8 kn[NS];
   auto load_k = [&](int kt) {
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) kn[s_] = gfrag<__bf16, true>(K, kt * 32 + r32, a.Nk, a.ks[1], a.D, s_, h);
+    for (int s_ = 0; s_ < NS; ++s_) kn[s_] = th2_frag(rK, kt * 32 + r32, a.ks[1], a.D, s_, h);
   };
   auto scores = [&](int kt) {
     bf16x8 kc[NS];
@@ -362,10 +373,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
     }
   };
   WStage<__bf16, DP, true> vst;   // V tile kt + 1 in flight while tile kt computes (wave-private image)
-  vst.load(V, 0, a.Nk, a.vs[1], a.D, lane);
+  vst.load_buf(rV, 0, a.vs[1], a.D, lane);
   vst.write(ldsV, lane);
   for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vst.load(V, (kt + 1) * 32, a.Nk, a.vs[1], a.D, lane);
+    if (kt + 1 < nkt) vst.load_buf(rV, (kt + 1) * 32, a.vs[1], a.D, lane);
     scores(kt);
     __syncthreads();
     probs(kt);
@@ -412,6 +423,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
+  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
+                               rV = row_rsrc(V, a.Nk, a.vs[1]), rG = row_rsrc(G, a.Nq, a.dos[1]);
 
   th2_zero_pad<KST>(XS, H, tid, 64 * H);
   th2_zero_pad<KST>(XG, H, tid, 64 * H);
@@ -420,9 +433,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   bf16x8 qf[NS], gf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    qf[s] = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s, h);
+    qf[s] = th2_frag(rQ, q, a.qs[1], a.D, s, h);
     if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
-    gf[s] = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s, h);
+    gf[s] = th2_frag(rG, q, a.dos[1], a.D, s, h);
   }
   const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);    // S1 = T1^T S        (image)
   const Th2Mix m2t = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
@@ -439,8 +452,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   auto load_kv = [&](int kt) {
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
-      kn[s_] = gfrag<__bf16, true>(K, kt * 32 + r32, a.Nk, a.ks[1], a.D, s_, h);
-      vn[s_] = gfrag<__bf16, true>(V, kt * 32 + r32, a.Nk, a.vs[1], a.D, s_, h);
+      kn[s_] = th2_frag(rK, kt * 32 + r32, a.ks[1], a.D, s_, h);
+      vn[s_] = th2_frag(rV, kt * 32 + r32, a.vs[1], a.D, s_, h);
     }
   };
   auto tiles = [&](int kt) {   // S_w -> XS, dP2_w -> XG
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   f32x4 dt1 = {0.f, 0.f, 0.f, 0.f};
   WStage<__bf16, DP, true> kst;
   for (int kt = 0; kt < nkt; ++kt) {
-    kst.load(K, kt * 32, a.Nk, a.ks[1], a.D, lane);
+    kst.load_buf(rK, kt * 32, a.ks[1], a.D, lane);
     tiles(kt);
     if (rot) kst.rope(a.rope, kt * 32, lane);
     kst.write(ldsK, lane);
@@ -613,6 +626,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
+  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
+                               rV = row_rsrc(V, a.Nk, a.vs[1]), rG = row_rsrc(G, a.Nq, a.dos[1]);
 
   th2_zero_pad<KST>(XS, H, tid, 64 * H);
   th2_zero_pad<KST>(XG, H, tid, 64 * H);
@@ -621,9 +636,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    kf[s] = gfrag<__bf16, true>(K, key, a.Nk, a.ks[1], a.D, s, h);
+    kf[s] = th2_frag(rK, key, a.ks[1], a.D, s, h);
     if (rot) kf[s] = rope8<1>(kf[s], a.rope, key, 16 * s + 8 * h);
-    vf[s] = gfrag<__bf16, true>(V, key, a.Nk, a.vs[1], a.D, s, h);
+    vf[s] = th2_frag(rV, key, a.vs[1], a.D, s, h);
   }
   if (w == 0) {
     Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
@@ -647,30 +662,32 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   char* bufQ = TWO ? buf + NWMAX * I::bytes(32) : buf;
   WStage<__bf16, DP, true> gst, qst;
   if constexpr (TWO) {
-    gst.load(G, 0, a.Nq, a.dos[1], a.D, lane);
-    qst.load(Q, 0, a.Nq, a.qs[1], a.D, lane);
+    gst.load_buf(rG, 0, a.dos[1], a.D, lane);
+    qst.load_buf(rQ, 0, a.qs[1], a.D, lane);
     if (rot) qst.rope(a.rope, 0, lane);
     gst.write(buf, lane);
     qst.write(bufQ, lane);
   }
   for (int qt = 0; qt < nqt; ++qt) {
     const int q = qt * 32 + r32;
-    if constexpr (TWO) {
-      if (qt + 1 < nqt) {
-        gst.load(G, (qt + 1) * 32, a.Nq, a.dos[1], a.D, lane);
-        qst.load(Q, (qt + 1) * 32, a.Nq, a.qs[1], a.D, lane);
-      }
-    } else {
-      gst.load(G, qt * 32, a.Nq, a.dos[1], a.D, lane);
-      qst.load(Q, qt * 32, a.Nq, a.qs[1], a.D, lane);
-    }
+    // this tile's row constants, raw (scaled / masked where used, after the barrier), issued
+    // BEFORE the next tile's Q / dO prefetch: waiting for them then leaves the prefetch in flight
+    // (vmcnt counts in order; loaded after it, the wait drained the prefetch every tile)
     float lse2[NR], dl[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      const int i = row_of(r, h);
-      const bool ok = i < H && q < a.Nq;
-      lse2[r] = ok ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
-      dl[r] = ok ? a.delta[((size_t)b * H + i) * a.Nq + q] : 0.f;
+      const size_t o = ((size_t)b * H + min(row_of(r, h), H - 1)) * a.Nq + min(q, a.Nq - 1);
+      lse2[r] = a.lse[o];
+      dl[r] = a.delta[o];
+    }
+    if constexpr (TWO) {
+      if (qt + 1 < nqt) {
+        gst.load_buf(rG, (qt + 1) * 32, a.dos[1], a.D, lane);
+        qst.load_buf(rQ, (qt + 1) * 32, a.qs[1], a.D, lane);
+      }
+    } else {
+      gst.load_buf(rG, qt * 32, a.dos[1], a.D, lane);
+      qst.load_buf(rQ, qt * 32, a.qs[1], a.D, lane);
     }
     {
       f32x16 s = zero16(), g = zero16();
@@ -681,9 +698,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
           qa = I::rowfrag(bufQ, r32, s_, h);
           ga = I::rowfrag(buf, r32, s_, h);
         } else {
-          qa = gfrag<__bf16, true>(Q, q, a.Nq, a.qs[1], a.D, s_, h);
+          qa = th2_frag(rQ, q, a.qs[1], a.D, s_, h);
           if (rot) qa = rope8<1>(qa, a.rope, q, 16 * s_ + 8 * h);
-          ga = gfrag<__bf16, true>(G, q, a.Nq, a.dos[1], a.D, s_, h);
+          ga = th2_frag(rG, q, a.dos[1], a.D, s_, h);
         }
         if (s_ < NS - 1 || full) {   // query rows, key lanes (th2_put)
           s = MF<__bf16>::mma(qa, kf[s_], s);
@@ -695,6 +712,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     }
     if constexpr (!TWO) gst.write(buf, lane);
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const bool ok = row_of(r, h) < H && q < a.Nq;
+      lse2[r] = ok ? lse2[r] * kLog2e : kInf;
+      dl[r] = ok ? dl[r] : 0.f;
+    }
     constexpr int G = 2;   // blocks (keys) per group: independent chains issued together
     for (int b0 = w; b0 < 32; b0 += G * H) {
       f32x16 p[G], dp[G];

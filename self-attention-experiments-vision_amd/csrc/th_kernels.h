@@ -109,6 +109,21 @@ template <typename T, int DP, bool VEC> struct WStage {
       }
     }
   }
+  // VEC bf16 path through a buffer descriptor over the valid rows (row_rsrc): rows past the end
+  // and columns >= D read as zero from the hardware range check.  The select-based load above
+  // makes hipcc branch around every load and wait vmcnt(0) after it, which turned the next
+  // tile's prefetch into a synchronous load (cdna_hip_programming.md §5, "three .s-level traps" (c)).
+  __device__ __forceinline__ void load_buf(__amdgpu_buffer_rsrc_t rsrc, int row0, long long rs, int D, int lane) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int id = lane + 64 * i;
+      const int r = id / CPR, c = id % CPR;
+      const unsigned off = (c * EPC < D && id < 32 * CPR)
+                               ? (unsigned)(((long long)(row0 + r) * rs + c * EPC) * (long long)sizeof(T))
+                               : 0x80000000u;
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+    }
+  }
   __device__ __forceinline__ void write(char* lds, int lane) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
