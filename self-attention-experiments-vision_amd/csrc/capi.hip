@@ -19,7 +19,6 @@
 #include "fwd2.h"
 #include "bwd2.h"
 #include "bwd3.h"
-#include "bwd3p.h"
 #include "cls.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
@@ -314,28 +313,6 @@ template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16> int bwd3
   if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>, C::LDS)) return rc;
   hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
   return check_launch("attn_bwd3");
-}
-
-// persistent single-pass backward (bwd3p.h): one workgroup per CU walking the (batch, head) units
-int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
-      n = 256;
-  }
-  return n;
-}
-template <int DP, int NSU = DP / 16> int bwd3p_run(hipStream_t st, const AttnArgs& a) {
-  using C = B3<DP, 8, 1>;
-  using P = B3P<DP, 8>;
-  if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3p: %d keys > %d", a.Nk, C::BK);
-  const long long units = (long long)a.H * a.B;
-  if (units > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  const int grid = (int)std::min<long long>(units, num_cus());
-  if (int rc = lds_attr((const void*)attn_bwd3p_kernel<DP, 8, NSU>, P::LDS)) return rc;
-  hipLaunchKernelGGL((attn_bwd3p_kernel<DP, 8, NSU>), dim3((unsigned)grid), dim3(512), P::LDS, st, a);
-  return check_launch("attn_bwd3p");
 }
 
 template <typename T, int DP, bool VEC, bool REL> struct BwdL {
@@ -739,11 +716,6 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     hipStream_t st = (hipStream_t)stream;
     if (a.Nk <= kB3Keys && var != 2 && var < 10 && dp <= 64) {
 #ifdef SAE_DEV_KNOBS
-      if (var == 20) {   // persistent bwd3 with the next unit's K / V prefetched by LDS-DMA
-        if (dp == 32) return bwd3p_run<32>(st, a);
-        if (dp == 64 && d->head_dim <= 48) return bwd3p_run<64, 3>(st, a);
-        if (dp == 64) return bwd3p_run<64>(st, a);
-      }
       if (var == 3) {   // four waves x two 32-key sub-blocks (one wave per SIMD): measured slower
         if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
         if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
@@ -1596,11 +1568,13 @@ const char* sae_build_info(void) { return "sae_attn gfx950 (" __DATE__ " " __TIM
 int sae_dev_stamps(void* dst, size_t bytes, int clear) {
   if (bytes > sizeof(unsigned long long) * (size_t)kStampRecs) return fail(SAE_EINVAL, "stamps: %zu bytes", bytes);
   hipError_t e;
-  if (clear) {
+  e = hipDeviceSynchronize();   // every stream: no kernel may be writing stamps meanwhile
+  if (e == hipSuccess && clear) {
     void* p = nullptr;
     e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_sae_stamps));
     if (e == hipSuccess) e = hipMemset(p, 0, sizeof(unsigned long long) * (size_t)kStampRecs);
-  } else {
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  } else if (e == hipSuccess) {
     e = hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_sae_stamps), bytes, 0, hipMemcpyDeviceToHost);
   }
   if (e != hipSuccess) return fail(SAE_EHIP, "stamps: %s", hipGetErrorString(e));
