@@ -731,26 +731,33 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);
 #ifdef SAE_DEV_KNOBS
-    if (var == 30 || var == 31) {
-      const hipError_t e = bwd2_agpr128(st, a, false, var - 30);
+    if (var == 30) {
+      const hipError_t e = bwd2_agpr128(st, a, false, 0);
       return e == hipSuccess ? ok() : fail(SAE_EHIP, "bwd2 agpr: %s", hipGetErrorString(e));
     }
+    if (var == 32) return bwd2_run<128, 4, 1, 4, 1>(st, a);
 #endif
-    // head_dim 128 (BoTNet): one wave per SIMD (the dK / dV accumulators of 32 keys x 128 columns
-    // plus the K / V fragments need more than half the register file)
-    return bwd2_run<128, 4, 1, 4, 1>(st, a);
+    // head_dim 128 (BoTNet): the dK / dV pass at one wave per SIMD (the dK / dV accumulators of 32
+    // keys x 128 columns plus the K / V fragments need more than half the register file), built in
+    // the AGPR translation unit (bwd_agpr.hip: accumulators in AGPRs, no spills; bot14 bwd
+    // 222 -> 216 us, bot7 49 -> 47 us same box, profiles/r03f_bot_agpr_ab.txt)
+    {
+      const hipError_t e = bwd2_agpr128(st, a, false, 1);
+      return e == hipSuccess ? ok() : fail(SAE_EHIP, "attn_bwd2 (head_dim 128): %s", hipGetErrorString(e));
+    }
   }
   if (var != 1 && d->dtype == SAE_DTYPE_BF16 && vec && rel && rel_lean(a)) {   // BoTNet relative logits
     const int dp = pick_dp(d->head_dim);
     hipStream_t st = (hipStream_t)stream;
     if (dp == 32) return bwd2_run<32, 4, 2, 4, 2, false, true>(st, a);
     if (dp == 64) return bwd2_run<64, 4, 2, 4, 1, false, true>(st, a);
-#ifdef SAE_DEV_KNOBS
-    if (var == 30 || var == 31) {
-      const hipError_t e = bwd2_agpr128(st, a, true, var - 30);
-      return e == hipSuccess ? ok() : fail(SAE_EHIP, "bwd2 agpr: %s", hipGetErrorString(e));
+    // head_dim 128 with relative logits: at 14 x 14 both passes at one wave per SIMD in the AGPR
+    // unit (the dQ pass's relative-logit state spills 75 VGPRs at two waves per SIMD): bot14+rel
+    // bwd 315 -> 298 us; the 7 x 7 grid keeps the two-wave dQ pass (59 vs 67 us)
+    if (a.Nk >= 128) {
+      const hipError_t e = bwd2_agpr128(st, a, true, 0);
+      return e == hipSuccess ? ok() : fail(SAE_EHIP, "attn_bwd2 (relpos, head_dim 128): %s", hipGetErrorString(e));
     }
-#endif
     return bwd2_run<128, 4, 2, 4, 1, false, true>(st, a);
   }
   return dispatch<BwdL>(d->dtype, pick_dp(d->head_dim), vec, rel, (hipStream_t)stream, a);
