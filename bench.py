@@ -278,6 +278,9 @@ def main():
                     help="N=1: a one-rank RCCL process group, so the overlapped bucket all-reduces run (captured "
                          "in the step's HIP graph) as they do at N > 1")
     ap.add_argument("--bucket-mb", type=float, default=25.0, help="gradient all-reduce bucket size")
+    ap.add_argument("--no-persistent-casts", action="store_true",
+                    help="cast every Dense kernel to bf16 at the start of each forward instead of the optimizer "
+                         "writing the bf16 copies in its update")
     args = ap.parse_args()
     if args.world1_rccl:
         os.environ["SAE_WORLD1_RCCL"] = "1"
@@ -310,7 +313,8 @@ def main():
     use_graph = not args.eager
     step = train.TrainStep(model, global_batch=B * world, device=dev, graph=use_graph, input_layout=args.input_layout,
                            flat_grads=False if args.no_flat_grads else None, grad_sinks=not args.no_grad_sinks,
-                           two_graphs=True if args.two_graphs else None, bucket_cap_mb=args.bucket_mb)
+                           two_graphs=True if args.two_graphs else None, bucket_cap_mb=args.bucket_mb,
+                           persistent_casts=not args.no_persistent_casts)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = torch.randn(B, args.img_size, args.img_size, 3, device=dev, generator=g)
     if args.input_layout == "HWCN":

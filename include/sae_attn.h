@@ -301,6 +301,32 @@ int sae_adamw_plan(int32_t n_items, float* const* p, const float* const* g, floa
 int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int32_t* step,
                    float lr, float beta1, float beta2, float eps, float weight_decay);
 
+/* The same update with the bf16 compute copies of the Dense kernels written by the optimizer pass
+   (the per-forward fp32 -> bf16 casts of Flax Dense, sae_weight_cast_multi, move into the
+   update): item i is a Dense kernel p[i] fp32 [K[i]][N[i]] (contiguous, gradient and moments laid
+   out alike) whose updated values are also stored as bf16 into columns col0[i] .. col0[i] + N[i]
+   of w16[i] [K][ld16[i]] and rows col0[i] .. of wt16[i] [*][ldT[i]] (either may be NULL).
+   sae_adamw_cast_plan (host only) cuts the items into 64 x 64 tiles (K, N, col0, ld16, ldT
+   multiples of 4; p / g / m / v 16-byte, w16 / wt16 8-byte aligned: SAE_EUNSUPPORTED otherwise);
+   sae_adamw_step_cast runs the chunk table (the other parameters) and the tile table in ONE launch
+   after the step-counter tick.  The parameter values are bit-identical to sae_adamw_step's. */
+typedef struct sae_adamw_cast_tile {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  void* w16;
+  void* wt16;
+  int32_t K, N, ld16, ldT, col0, k0, n0, pad;
+} sae_adamw_cast_tile;
+int sae_adamw_cast_plan(int32_t n_items, float* const* p, const float* const* g, float* const* m,
+                        float* const* v, const int32_t* K, const int32_t* N, void* const* w16,
+                        const int32_t* ld16, void* const* wt16, const int32_t* ldT, const int32_t* col0,
+                        sae_adamw_cast_tile* tiles, int64_t max_tiles, int64_t* n_tiles);
+int sae_adamw_step_cast(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int64_t n_tiles,
+                        const sae_adamw_cast_tile* tiles, int32_t* step, float lr, float beta1, float beta2,
+                        float eps, float weight_decay);
+
 /* Encoder input of ViT / DeiT (models/vit.py:82-85 class-token concatenate, vit.py:46 +
    position_embed.py:48 AddAbsPosEmbed), tokens bf16 [B][L][E] from the patch embedding, cls fp32
    [E], pos fp32 [L+1][E]:  x fp32 [B][L+1][E] = concat(cls, float(tokens)) + pos.  Backward:

@@ -83,6 +83,8 @@ _PROTOS = [
     ("sae_layernorm_bwd_scaled", _i32, [_vp, _i32, _i32] + [_vp] * 14 + [_i32, _vp]),
     ("sae_adamw_plan", _i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     ("sae_adamw_step", _i32, [_vp, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32]),
+    ("sae_adamw_cast_plan", _i32, [_i32] + [_vp] * 11 + [_vp, _i64, _vp]),
+    ("sae_adamw_step_cast", _i32, [_vp, _i64, _vp, _i64, _vp, _vp, _f32, _f32, _f32, _f32, _f32]),
     ("sae_tokens_fwd", _i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     ("sae_tokens_bwd", _i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     ("sae_smoothed_ce_fwd", _i32, [_vp, _i32, _i32, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp]),
@@ -107,6 +109,13 @@ class AdamwChunk(ctypes.Structure):
     """Mirror of ``sae_adamw_chunk`` (include/sae_attn.h)."""
     _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
                 ("n", ctypes.c_int32), ("vec", ctypes.c_int32)]
+
+
+class AdamwCastTile(ctypes.Structure):
+    """Mirror of ``sae_adamw_cast_tile`` (include/sae_attn.h)."""
+    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("w16", ctypes.c_void_p), ("wt16", ctypes.c_void_p)] + \
+        [(f, ctypes.c_int32) for f in ("K", "N", "ld16", "ldT", "col0", "k0", "n0", "pad")]
 
 
 SAE_ADAMW_CHUNK = 2048

@@ -1511,6 +1511,71 @@ int sae_adamw_step(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks
   return check_launch("adamw");
 }
 
+static_assert(sizeof(sae_adamw_cast_tile) == sizeof(AdamwCastTile), "sae_adamw_cast_tile mirrors AdamwCastTile");
+
+int sae_adamw_cast_plan(int32_t n_items, float* const* p, const float* const* g, float* const* m,
+                        float* const* v, const int32_t* K, const int32_t* N, void* const* w16, const int32_t* ld16,
+                        void* const* wt16, const int32_t* ldT, const int32_t* col0, sae_adamw_cast_tile* tiles,
+                        int64_t max_tiles, int64_t* n_tiles) {
+  if (n_items < 0 || !n_tiles || (n_items > 0 && (!p || !g || !m || !v || !K || !N || !col0)))
+    return fail(SAE_EINVAL, "adamw_cast_plan: bad arguments");
+  const auto a8 = [](const void* q) { return ((uintptr_t)q & 7) == 0; };
+  int64_t k = 0;
+  for (int32_t i = 0; i < n_items; ++i) {
+    void* o16 = w16 ? w16[i] : nullptr;
+    void* oT = wt16 ? wt16[i] : nullptr;
+    const int32_t l16 = ld16 ? ld16[i] : 0, lT = ldT ? ldT[i] : 0;
+    if (!p[i] || !g[i] || !m[i] || !v[i] || K[i] < 1 || N[i] < 1 || col0[i] < 0 || (!o16 && !oT) ||
+        (o16 && l16 < col0[i] + N[i]) || (oT && lT < K[i]))
+      return fail(SAE_EINVAL, "adamw_cast_plan: item %d invalid (K %d N %d col0 %d ld16 %d ldT %d)", i, K[i], N[i],
+                  col0[i], l16, lT);
+    if (K[i] % 4 || N[i] % 4 || col0[i] % 4 || !aligned16(p[i]) || !aligned16(g[i]) || !aligned16(m[i]) ||
+        !aligned16(v[i]) || (o16 && (l16 % 4 || !a8(o16))) || (oT && (lT % 4 || !a8(oT))))
+      return fail(SAE_EUNSUPPORTED, "adamw_cast_plan: item %d needs K/N/col0/ld multiples of 4 and aligned buffers",
+                  i);
+    for (int32_t k0 = 0; k0 < K[i]; k0 += 64)
+      for (int32_t n0 = 0; n0 < N[i]; n0 += 64, ++k) {
+        if (k < max_tiles && tiles) {
+          sae_adamw_cast_tile& t = tiles[k];
+          t.p = p[i];
+          t.g = g[i];
+          t.m = m[i];
+          t.v = v[i];
+          t.w16 = o16;
+          t.wt16 = oT;
+          t.K = K[i];
+          t.N = N[i];
+          t.ld16 = l16;
+          t.ldT = lT;
+          t.col0 = col0[i];
+          t.k0 = k0;
+          t.n0 = n0;
+          t.pad = 0;
+        }
+      }
+  }
+  *n_tiles = k;
+  if (k > max_tiles)
+    return fail(SAE_EINVAL, "adamw_cast_plan: %lld tiles > capacity %lld", (long long)k, (long long)max_tiles);
+  return ok();
+}
+
+int sae_adamw_step_cast(void* stream, int64_t n_chunks, const sae_adamw_chunk* chunks, int64_t n_tiles,
+                        const sae_adamw_cast_tile* tiles, int32_t* step, float lr, float beta1, float beta2, float eps,
+                        float weight_decay) {
+  if (n_chunks < 0 || n_tiles < 0 || n_chunks + n_tiles >= (1LL << 31) || (n_chunks > 0 && !chunks) ||
+      (n_tiles > 0 && !tiles) || !step)
+    return fail(SAE_EINVAL, "adamw_step_cast: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adamw_tick_kernel, dim3(1), dim3(64), 0, st, step);
+  if (int rc = check_launch("adamw_tick")) return rc;
+  if (n_chunks + n_tiles == 0) return ok();
+  hipLaunchKernelGGL(adamw_cast_kernel, dim3((unsigned)(n_chunks + n_tiles)), dim3(256), 0, st,
+                     reinterpret_cast<const AdamwChunk*>(chunks), (int)n_chunks,
+                     reinterpret_cast<const AdamwCastTile*>(tiles), step, lr, beta1, beta2, eps, weight_decay);
+  return check_launch("adamw_cast");
+}
+
 static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const float* mean, const float* rstd,
                        const float* gamma, const void* dy, const float* dxin, float* dx, void* ddelta,
                        float* dgamma, float* dbeta, void* workspace, const void* delta, const float* lsc,

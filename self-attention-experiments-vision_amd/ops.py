@@ -618,14 +618,13 @@ def cast_weights(groups) -> None:
         K = ws[0].shape[0]
         if any(w.dim() != 2 or w.shape[0] != K or w.dtype != torch.float32 or not w.is_contiguous() for w in ws):
             continue
+        if _wkey(ws) in _PERSIST:   # the optimizer keeps this group's copies
+            continue
         dev = ws[0].device
         N = sum(w.shape[1] for w in ws)
         w16 = torch.empty((K, N), dtype=torch.bfloat16, device=dev)
         wt16 = torch.empty((N, K), dtype=torch.bfloat16, device=dev)
-        col = 0
-        for w in ws:
-            items.append(L.WeightCastItem(w.data_ptr(), w16.data_ptr(), wt16.data_ptr(), K, w.shape[1], N, K, col))
-            col += w.shape[1]
+        items += _cast_items(ws, w16, wt16)
         _WCACHE[_wkey(ws)] = (tuple(w._version for w in ws), w16, wt16)
     if items:
         arr = (L.WeightCastItem * len(items))(*items)
@@ -636,8 +635,64 @@ def clear_weight_cache() -> None:
     _WCACHE.clear()
 
 
+# ---------------------------------------------------------- persistent bf16 weight copies
+# Groups whose bf16 copies the optimizer writes (FusedAdamW with cast_groups: the update and the
+# cast in one pass, sae_adamw_step_cast) stay registered across steps: the forward neither casts
+# nor allocates for them.  An in-place change of a weight OUTSIDE the optimizer (load_state_dict,
+# a copy_) bumps its version counter; the next lookup then re-casts into the same buffers.  The
+# optimizer writes through raw pointers (no version bump) and calls ``persistent_casts_fresh``
+# whenever it rewrites the copies itself.
+_PERSIST = {}
+
+
+def register_persistent_casts(groups, w16s, wt16s) -> None:
+    for ws, w16, wt16 in zip(groups, w16s, wt16s):
+        _PERSIST[_wkey(ws)] = [tuple(w._version for w in ws), w16, wt16, list(ws)]
+
+
+def unregister_persistent_casts(groups) -> None:
+    for ws in groups:
+        _PERSIST.pop(_wkey(ws), None)
+
+
+def persistent_casts_fresh(groups) -> None:
+    """The copies of ``groups`` match their fp32 weights as of now."""
+    for ws in groups:
+        e = _PERSIST.get(_wkey(ws))
+        if e is not None:
+            e[0] = tuple(w._version for w in ws)
+
+
+def _cast_items(ws, w16, wt16):
+    K, N = ws[0].shape[0], w16.shape[1]
+    items, col = [], 0
+    for w in ws:
+        items.append(L.WeightCastItem(w.data_ptr(), w16.data_ptr(), wt16.data_ptr(), K, w.shape[1], N, K, col))
+        col += w.shape[1]
+    return items
+
+
+def recast_persistent(groups) -> None:
+    """Re-cast the registered copies of ``groups`` from their fp32 weights (one launch)."""
+    items = []
+    for ws in groups:
+        e = _PERSIST.get(_wkey(ws))
+        if e is not None:
+            items += _cast_items(e[3], e[1], e[2])
+            e[0] = tuple(w._version for w in e[3])
+    if items:
+        arr = (L.WeightCastItem * len(items))(*items)
+        L.check(L.load().sae_weight_cast_multi(_stream(groups[0][0]), len(items), arr))
+
+
 def _cast_lookup(ws):
-    e = _WCACHE.get(_wkey(ws))
+    key = _wkey(ws)
+    e = _PERSIST.get(key)
+    if e is not None:
+        if e[0] != tuple(w._version for w in ws):
+            recast_persistent([ws])
+        return e[1], e[2]
+    e = _WCACHE.get(key)
     if e is not None and e[0] == tuple(w._version for w in ws):
         return e[1], e[2]
     return None

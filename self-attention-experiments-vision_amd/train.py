@@ -94,12 +94,19 @@ class FusedAdamW:
     parameters whose gradients live in one flat buffer: every parameter in one HIP launch
     (``sae_adamw_step``, csrc/adamw.h) instead of torch's multi-tensor launches.  The moments are
     two more flat buffers laid out like the gradients; the step counter stays on the device, so the
-    update can be captured in a HIP graph and replayed."""
+    update can be captured in a HIP graph and replayed.
+
+    ``cast_groups``: column-stacked groups of 2-D fp32 Dense kernels (the ``ops.cast_weights``
+    groups; each kernel a whole parameter, possibly reshaped) whose bf16 compute copies the
+    update writes as it goes (``sae_adamw_step_cast``): the forward then reads persistent copies
+    (``ops.register_persistent_casts``) instead of casting every weight at its start.  Parameter
+    values are bit-identical either way."""
 
     def __init__(self, params, flat_grad: torch.Tensor, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0):
+                 weight_decay: float = 0.0, cast_groups=None):
         import ctypes
         from . import _lib as L
+        from . import ops
         self.lib = L.load()
         self.params = list(params)
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
@@ -107,32 +114,99 @@ class FusedAdamW:
         self.m = torch.zeros_like(flat_grad)
         self.v = torch.zeros_like(flat_grad)
         self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
-        n = len(self.params)
-        P = (ctypes.c_void_p * n)()
-        G, M, V = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
-        N = (ctypes.c_int64 * n)()
+        slot = {}
         for i, p in enumerate(self.params):
             g = p.grad
             if (p.dtype != torch.float32 or not p.is_contiguous() or g is None or g.dtype != torch.float32
                     or not g.is_contiguous() or g.data_ptr() < flat_grad.data_ptr()):
                 raise ValueError("FusedAdamW: fp32 contiguous parameters with views of the flat gradient buffer")
             off = (g.data_ptr() - flat_grad.data_ptr()) // 4
-            P[i], G[i] = p.data_ptr(), g.data_ptr()
-            M[i], V[i] = self.m.data_ptr() + 4 * off, self.v.data_ptr() + 4 * off
-            N[i] = p.numel()
-        cap = sum((p.numel() + L.SAE_ADAMW_CHUNK - 1) // L.SAE_ADAMW_CHUNK for p in self.params)
+            slot[p.data_ptr()] = (i, p, g.data_ptr(), self.m.data_ptr() + 4 * off, self.v.data_ptr() + 4 * off)
+        # the Dense kernels whose copies the update writes: whole parameters, shapes / alignment
+        # the tile path takes (K, N, column offsets multiples of 4)
+        self.cast_groups, self.copies = [], []
+        tiles_in = []
+        for ws in (cast_groups or []):
+            K = ws[0].shape[0]
+            ent = [slot.get(w.data_ptr()) for w in ws]
+            if (any(e is None or e[1].numel() != w.numel() for e, w in zip(ent, ws))
+                    or any(w.dim() != 2 or w.shape[0] != K for w in ws)
+                    or K % 4 or any(w.shape[1] % 4 for w in ws)
+                    or any(e[2] % 16 or e[3] % 16 or e[4] % 16 or e[1].data_ptr() % 16 for e in ent)):
+                continue
+            N = sum(w.shape[1] for w in ws)
+            w16 = torch.empty((K, N), dtype=torch.bfloat16, device=dev)
+            wt16 = torch.empty((N, K), dtype=torch.bfloat16, device=dev)
+            col = 0
+            for e, w in zip(ent, ws):
+                tiles_in.append((e, K, w.shape[1], w16, wt16, N, col))
+                col += w.shape[1]
+            self.cast_groups.append(list(ws))
+            self.copies.append((w16, wt16))
+        in_tiles = {e[0] for e, *_ in tiles_in}
+        flat_idx = [i for i in range(len(self.params)) if i not in in_tiles]
+        n = len(flat_idx)
+        P = (ctypes.c_void_p * max(1, n))()
+        G, M, V = (ctypes.c_void_p * max(1, n))(), (ctypes.c_void_p * max(1, n))(), (ctypes.c_void_p * max(1, n))()
+        Nn = (ctypes.c_int64 * max(1, n))()
+        for j, i in enumerate(flat_idx):
+            p = self.params[i]
+            _, _, G[j], M[j], V[j] = slot[p.data_ptr()]
+            P[j], Nn[j] = p.data_ptr(), p.numel()
+        cap = sum((self.params[i].numel() + L.SAE_ADAMW_CHUNK - 1) // L.SAE_ADAMW_CHUNK for i in flat_idx)
         table = (L.AdamwChunk * max(1, cap))()
         cnt = ctypes.c_int64(0)
-        L.check(self.lib.sae_adamw_plan(n, P, G, M, V, N, table, cap, ctypes.byref(cnt)))
+        L.check(self.lib.sae_adamw_plan(n, P, G, M, V, Nn, table, cap, ctypes.byref(cnt)))
         self.n_chunks = int(cnt.value)
         self.table = torch.frombuffer(bytearray(table), dtype=torch.uint8).to(dev)   # device copy, built once
+        self.n_tiles = 0
+        self.tiles = None
+        if tiles_in:
+            k = len(tiles_in)
+            arr = lambda t: (t * k)()
+            P, G, M, V, W16, WT = (arr(ctypes.c_void_p) for _ in range(6))
+            Kx, Nx, LD, LT, C0 = (arr(ctypes.c_int32) for _ in range(5))
+            for j, (e, K, Nw, w16, wt16, Ntot, col) in enumerate(tiles_in):
+                P[j], G[j], M[j], V[j] = e[1].data_ptr(), e[2], e[3], e[4]
+                W16[j], WT[j] = w16.data_ptr(), wt16.data_ptr()
+                Kx[j], Nx[j], LD[j], LT[j], C0[j] = K, Nw, Ntot, K, col
+            cap = sum(-(-K // 64) * -(-Nw // 64) for _, K, Nw, *_ in tiles_in)
+            ttab = (L.AdamwCastTile * cap)()
+            L.check(self.lib.sae_adamw_cast_plan(k, P, G, M, V, Kx, Nx, W16, LD, WT, LT, C0, ttab, cap,
+                                                 ctypes.byref(cnt)))
+            self.n_tiles = int(cnt.value)
+            self.tiles = torch.frombuffer(bytearray(ttab), dtype=torch.uint8).to(dev)
+            ops.register_persistent_casts(self.cast_groups, [c[0] for c in self.copies], [c[1] for c in self.copies])
+            ops.recast_persistent(self.cast_groups)   # the copies of the initial weights
+            # the registry holds the weights (their addresses cannot be reused while registered);
+            # it lets go of them with the optimizer
+            import weakref
+            weakref.finalize(self, ops.unregister_persistent_casts, list(self.cast_groups))
 
     def step(self):
         from . import _lib as L
         b1, b2 = self.betas
         st = torch.cuda.current_stream(self.m.device).cuda_stream
-        L.check(self.lib.sae_adamw_step(st, self.n_chunks, self.table.data_ptr(), self.step_count.data_ptr(),
-                                        self.lr, b1, b2, self.eps, self.weight_decay))
+        if self.n_tiles:
+            L.check(self.lib.sae_adamw_step_cast(st, self.n_chunks, self.table.data_ptr(), self.n_tiles,
+                                                 self.tiles.data_ptr(), self.step_count.data_ptr(), self.lr, b1, b2,
+                                                 self.eps, self.weight_decay))
+        else:
+            L.check(self.lib.sae_adamw_step(st, self.n_chunks, self.table.data_ptr(), self.step_count.data_ptr(),
+                                            self.lr, b1, b2, self.eps, self.weight_decay))
+
+    def refresh_casts(self):
+        """Re-cast the copies after the parameters were overwritten outside the update."""
+        if self.cast_groups:
+            from . import ops
+            ops.recast_persistent(self.cast_groups)
+
+    def close(self):
+        """Stop serving the copies (the forward casts per call again)."""
+        if self.cast_groups:
+            from . import ops
+            ops.unregister_persistent_casts(self.cast_groups)
+            self.cast_groups = []
 
     def state_tensors(self):
         return [self.m, self.v, self.step_count]
@@ -149,7 +223,7 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
                  label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
                  graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None,
-                 grad_sinks: bool = True, two_graphs: Optional[bool] = None):
+                 grad_sinks: bool = True, two_graphs: Optional[bool] = None, persistent_casts: bool = True):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
@@ -215,7 +289,9 @@ class TrainStep:
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         self.opt = None
         if self.flat and on_gpu and all(p.dtype == torch.float32 and p.is_contiguous() for p in params):
-            self.opt = FusedAdamW(params, self._flat, **kw)
+            # the bf16 Dense copies written by the update (models that name them, bf16 compute)
+            groups = model.cast_groups() if persistent_casts and hasattr(model, "cast_groups") else None
+            self.opt = FusedAdamW(params, self._flat, cast_groups=groups, **kw)
         else:
             if self.graph:
                 kw["capturable"] = True   # step counters on the device: replayable
@@ -416,6 +492,7 @@ class TrainStep:
             if fused:
                 for t, v in zip(self.opt.state_tensors(), snap_fused):
                     t.copy_(v)
+                self.opt.refresh_casts()   # the bf16 copies of the restored weights
             for p in ([] if fused else params):
                 st = self.opt.state.get(p)
                 if not st:

@@ -184,6 +184,16 @@ class ViT(nn.Module):
         self.Encoder_0 = Encoder(n, embed_dim, num_layers, num_heads, expand_ratio, dtype, device)
         self.Dense_0 = Dense(embed_dim, num_classes, zero_init=True, device=device)
 
+    def cast_groups(self):
+        """Every Dense kernel the bf16 forward reads as a bf16 copy (the encoder's column-block
+        groups, the patch embedding, the head): the optimizer may keep these copies
+        (FusedAdamW ``cast_groups``).  None when the model computes in fp32."""
+        if self.dtype != torch.bfloat16:
+            return None
+        blocks = [getattr(self.Encoder_0, f"EncoderBlock_{i}") for i in range(self.Encoder_0.num_layers)]
+        return (encoder_weight_groups(blocks) + [[self.PatchEmbedBlock_0.Dense_0.kernel]] +
+                [[self.Dense_0.kernel]])
+
     def forward(self, inputs: torch.Tensor, is_training: bool, layout: str = "NHWC") -> torch.Tensor:
         """``layout`` "HWCN": ``inputs`` is the train-step feed [H, W, C, B] (train.py:80)."""
         x = patch_tokens(self.PatchEmbedBlock_0, inputs, self.patch_shape, self.dtype, layout)

@@ -193,3 +193,79 @@ def test_world1_rccl_overlapped_step(dev, model):
         dist.destroy_process_group()
         from sae_vision_amd import ops
         ops.set_sink_listener(None)
+
+
+def test_fused_adamw_cast_copies(dev):
+    """sae_adamw_step_cast: parameters bit-identical to sae_adamw_step's, and the bf16 copies the
+    update writes (plain [K, sum N] at the column offsets and its transpose) equal to the bf16
+    cast of the updated fp32 weights; partial 64 x 64 edge tiles (K 68, N 100) included, one
+    parameter outside every group (the flat chunk path in the same launch)."""
+    from sae_vision_amd import ops, train
+    g = torch.Generator(device=dev).manual_seed(13)
+    shapes = [(68, 100), (68, 36), (384, 1152), (7,), (256, 68)]
+    base = [torch.randn(s, device=dev, generator=g) for s in shapes]
+
+    def make():
+        ps = [t.clone().requires_grad_(True) for t in base]
+        offs, n = train.flat_layout(ps)
+        flat = torch.zeros(n, device=dev)
+        for p, o in zip(ps, offs):
+            p.grad = flat[o:o + p.numel()].view_as(p)
+        return ps, flat
+
+    a, fa = make()
+    b, fb = make()
+    kw = dict(lr=3e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
+    groups = [[b[0], b[1]], [b[2]], [b[4]]]
+    opt_a = train.FusedAdamW(a, fa, **kw)
+    opt_b = train.FusedAdamW(b, fb, cast_groups=groups, **kw)
+    try:
+        assert len(opt_b.cast_groups) == 3 and opt_b.n_tiles == 2 * 2 + 2 * 1 + 6 * 18 + 4 * 2
+        for _ in range(4):
+            for p, q in zip(a, b):
+                gr = torch.randn(p.shape, device=dev, generator=g)
+                p.grad.copy_(gr)
+                q.grad.copy_(gr)
+            opt_a.step()
+            opt_b.step()
+        torch.cuda.synchronize()
+        for p, q in zip(a, b):
+            assert torch.equal(p, q)
+        for ws, (w16, wt16) in zip(groups, opt_b.copies):
+            ref = torch.cat([w.detach() for w in ws], dim=1).to(torch.bfloat16)
+            assert torch.equal(w16, ref) and torch.equal(wt16, ref.t().contiguous())
+            assert ops._cast_lookup(ws)[0] is w16          # served to the forward as is
+        # an in-place change outside the optimizer is noticed: the next lookup re-casts
+        with torch.no_grad():
+            b[2].mul_(0.5)
+        w16, wt16 = ops._cast_lookup([b[2]])
+        torch.cuda.synchronize()
+        assert torch.equal(w16, b[2].detach().to(torch.bfloat16))
+    finally:
+        opt_b.close()
+    assert ops._wkey([b[2]]) not in ops._PERSIST
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_train_step_persistent_casts_bitwise(dev, graph):
+    """DeiT-Ti training steps with the optimizer writing the bf16 Dense copies (no cast in the
+    forward) give the same losses and parameters, bit for bit, as steps that cast every forward."""
+    from sae_vision_amd import ops, train, vit
+    torch.manual_seed(0)
+    m_a = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
+    m_b = copy.deepcopy(m_a)
+    s_a = train.TrainStep(m_a, global_batch=8, device=dev, graph=graph, persistent_casts=False)
+    s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=graph)
+    assert not s_a.opt.cast_groups
+    assert len(s_b.opt.cast_groups) == len(m_b.cast_groups())   # every Dense kernel of DeiT-Ti
+    g = torch.Generator(device=dev).manual_seed(3)
+    data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
+             torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
+    try:
+        la = [float(s_a(x, y)) for x, y in data]
+        lb = [float(s_b(x, y)) for x, y in data]
+        assert la == lb, (la, lb)
+        for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
+            assert torch.equal(pa, pb), n
+    finally:
+        s_b.opt.close()
