@@ -526,10 +526,10 @@ static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hip
   return 0;
 }
 
-// one sae_gemm_nt launch: 128 x 128 tiles, two LDS stage buffers of BK-deep A and B images
+// one sae_gemm_nt launch: TM x 128 tiles, two LDS stage buffers of BK-deep A and B images
 template <int EPI, class AL>
 static int nt_launch(const NtArgs& g, long long grid, hipStream_t st) {
-  const size_t lds = 4 * kNtT * NtDepth<AL>::value * 2;
+  const size_t lds = 2 * (NtRows<AL>::value + kNtT) * NtDepth<AL>::value * 2;
   if (int rc = lds_attr((const void*)gemm_nt_kernel<EPI, AL>, lds)) return rc;
   hipLaunchKernelGGL((gemm_nt_kernel<EPI, AL>), dim3((unsigned)grid), dim3(256), lds, st, g);
   return 0;
@@ -559,7 +559,8 @@ void sae_attn_desc_init(sae_attn_desc* d, int32_t batch, int32_t heads, int32_t 
 static int rope_check(const sae_attn_desc* d, const float* sin_tab, const float* cos_tab) {
   if (!sin_tab || !cos_tab) return fail(SAE_EINVAL, "rotary: sin_tab / cos_tab must be non-NULL");
   if (!aligned16(sin_tab) || !aligned16(cos_tab)) return fail(SAE_EINVAL, "rotary: tables must be 16-byte aligned");
-  if (d->head_dim % 8) return fail(SAE_EUNSUPPORTED, "rotary: fused rotary needs head_dim %% 8 == 0 (got %d)", d->head_dim);
+  if (d->head_dim % 8 || d->head_dim > 64)
+    return fail(SAE_EUNSUPPORTED, "rotary: fused rotary needs head_dim %% 8 == 0 and <= 64 (got %d)", d->head_dim);
   return SAE_OK;
 }
 static RopeTab make_rope(const sae_attn_desc* d, const float* sin_tab, const float* cos_tab) {
@@ -1059,8 +1060,8 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
     return fail(SAE_EINVAL, "gemm_nt: the GELU-derivative epilogue needs aux (ldaux >= N, multiple of 8) and no bias");
   if (!aligned16(a) || !aligned16(bt) || !aligned16(c) || !aligned16(c2) || !aligned16(aux) || !aligned16(bias))
     return fail(SAE_EINVAL, "gemm_nt: a, bt, c, c2, aux and bias must be 16-byte aligned");
-  if ((long long)kNtT * std::max(lda, ldb) * 2 >= (1LL << 31))
-    return fail(SAE_EUNSUPPORTED, "gemm_nt: a 128-row block exceeds 32-bit buffer addressing");
+  if (256LL * std::max(lda, ldb) * 2 >= (1LL << 31))
+    return fail(SAE_EUNSUPPORTED, "gemm_nt: a 256-row block exceeds 32-bit buffer addressing");
   NtArgs g;
   memset(&g, 0, sizeof g);
   g.a = reinterpret_cast<const __bf16*>(a);
@@ -1077,13 +1078,30 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   g.ldc = ldc;
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
-  const long long grid = (long long)((M + kNtT - 1) / kNtT) * ((N + kNtT - 1) / kNtT);
+  // tile height: 256 tokens for the GELU / GELU' epilogue GEMMs at K >= 768 (the ViT-B FF block:
+  // the epilogue's VALU work per output is amortised over twice the MFMA work per tile;
+  // tools/nt_probe.py at M 36928 K 768 N 3072: GELU 512 -> 634, GELU' 548 -> 609 TF/s) when that
+  // still gives >= 2 tiles per CU; 128 otherwise (plain GEMMs: no gain, profiles/r03n_nt_probe.txt)
+  const long long tn = (N + kNtT - 1) / kNtT;
+  bool tall = epilogue != SAE_EPI_NONE && K >= 768 && (long long)((M + 255) / 256) * tn >= 512;
+#ifdef SAE_DEV_KNOBS
+  if (int v = dev_knob("SAE_NT_VARIANT")) tall = v == 2;
+#endif
+  const int TM = tall ? 256 : kNtT;
+  const long long grid = (long long)((M + TM - 1) / TM) * tn;
   if (grid >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "gemm_nt: grid too large");
   // stage depth: the GELU / GELU' epilogue GEMMs at reduction depth <= 384 (DeiT-S / CaiT FF
   // block) run 32-deep stages (32 KiB of LDS: 3-4 workgroups per CU, so one tile's epilogue VALU
   // overlaps other tiles' MFMAs; same-box step A/B 9.19 -> 9.10 ms); deeper reductions (ViT-B,
   // K 768) and the plain GEMM keep 64-deep stages (2 workgroups per CU), which are faster there
   const bool shallow = K <= 384;
+  if (tall) {
+    const int rc = epilogue == SAE_EPI_NONE ? nt_launch<kEpiNone, NtRowAT<32, 256>>(g, grid, st)
+                   : epilogue == SAE_EPI_GELU ? nt_launch<kEpiGelu, NtRowAT<32, 256>>(g, grid, st)
+                                              : nt_launch<kEpiDGelu, NtRowAT<32, 256>>(g, grid, st);
+    if (rc) return rc;
+    return check_launch("gemm_nt");
+  }
   switch (epilogue) {
     case SAE_EPI_NONE:
       if (int rc = nt_launch<kEpiNone, NtRowAT<64>>(g, grid, st)) return rc;

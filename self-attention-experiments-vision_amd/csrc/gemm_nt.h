@@ -89,10 +89,10 @@ __device__ __forceinline__ unsigned dgelu_bf2(unsigned dw, unsigned hw) {   // d
   return f2_to_bf2(bf2_to_f2(dw) * ((x * q) * poly + s));
 }
 
-// one operand's 128 x BK stage: 16 * BK 16-byte chunks, BK / 16 per thread
-template <int BK> struct NtStageT {
+// one operand's ROWS x BK stage: ROWS * BK / 8 16-byte chunks, ROWS * BK / 2048 per thread
+template <int BK, int ROWS = 128> struct NtStageT {
   static constexpr int CPR = BK / 8;         // 16-byte chunks per row
-  static constexpr int PER = 128 * CPR / 256;
+  static constexpr int PER = ROWS * CPR / 256;
   uint4 v[PER];
   unsigned goff[PER];
   unsigned loff[PER];
@@ -117,15 +117,15 @@ template <int BK> struct NtStageT {
 };
 using NtStage = NtStageT<kNtK>;
 
-// A-operand loader of the plain GEMM: rows m0 .. m0 + 127 of the row-major a [M][K] through a
-// buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders (64-deep
-// stages); a loader also maps GEMM row m to its output row (orow).
-template <int BK> struct NtRowAT {
+// A-operand loader of the plain GEMM: rows m0 .. m0 + ROWS - 1 of the row-major a [M][K] through
+// a buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders (64-deep
+// stages, 128 rows); a loader also maps GEMM row m to its output row (orow).
+template <int BK, int ROWS = 128> struct NtRowAT {
   static constexpr int kBK = BK;
-  NtStageT<BK> s;
+  NtStageT<BK, ROWS> s;
   __amdgpu_buffer_rsrc_t rs;
   __device__ __forceinline__ void init(const NtArgs& a, int tid, int m0) {
-    rs = row_rsrc(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
+    rs = row_rsrc(a.a + (long long)m0 * a.lda, min(ROWS, a.M - m0), a.lda);
     s.init(tid, a.lda);
   }
   __device__ __forceinline__ void load(const NtArgs&, int st) { s.load(rs, (unsigned)st * (BK * 2)); }
@@ -135,20 +135,37 @@ template <int BK> struct NtRowAT {
 using NtRowA = NtRowAT<kNtK>;
 
 template <class AL> struct NtDepth { static constexpr int value = kNtK; };
-template <int BK> struct NtDepth<NtRowAT<BK>> { static constexpr int value = BK; };
+template <int BK, int ROWS> struct NtDepth<NtRowAT<BK, ROWS>> { static constexpr int value = BK; };
+template <class AL> struct NtRows { static constexpr int value = kNtT; };
+template <int BK, int ROWS> struct NtRows<NtRowAT<BK, ROWS>> { static constexpr int value = ROWS; };
+
+// Tiles: TM (128 or 256) tokens x 128 features per workgroup, each wave TM / 2 tokens x 64
+// features (UM = TM / 64 token sub-tiles of 32).  The 256-token tile reads 6 fragments from LDS
+// per 8 MFMAs instead of 4 per 4 (43 vs 32 flop per LDS byte: the 128-token tile saturates LDS
+// bandwidth before the MFMA pipe) and fetches the weight once per 256 tokens; it runs 32-deep
+// stages so that the two staged register sets still fit beside the 128 accumulator registers.
+template <int EPI, class AL>
+constexpr int nt_min_blocks() {
+  return NtRows<AL>::value == 256 ? 2 : NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ? 3 : 4) : 2;
+}
 
 template <int EPI, class AL = NtRowA>
-__global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ? 3 : 4) : 2) void gemm_nt_kernel(NtArgs a) {
+__global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kernel(NtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BK = NtDepth<AL>::value;   // K per stage
-  constexpr int IMG = kNtT * BK * 2;       // one operand image (16 KiB at BK = 64)
+  constexpr int TM = NtRows<AL>::value;    // tokens per tile
+  constexpr int UM = TM / 64;              // 32-token sub-tiles per wave
+  constexpr int IMGA = TM * BK * 2;        // A image (16 KiB at 128 x 64)
+  constexpr int IMG = kNtT * BK * 2;       // B image
+  constexpr int BUF = IMGA + IMG;
   const int tn = (a.N + kNtT - 1) / kNtT;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / tn, nt = bid % tn;
-  const int m0 = mt * kNtT, n0 = nt * kNtT;
+  const int m0 = mt * TM, n0 = nt * kNtT;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w & 1, wn = w >> 1;   // this wave's 64 (tokens) x 64 (features) quarter
+  const int wm = w & 1, wn = w >> 1;   // this wave's TM / 2 (tokens) x 64 (features) quarter
+  constexpr int WT = TM / 2;
 
   // rows past N read zero through the descriptor's range check
   const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
@@ -173,56 +190,63 @@ __global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ?
   // main loop, so their HBM traffic overlaps the MFMAs instead of following them
   const int c8 = lane & 7;                 // 16-byte chunk of an epilogue row segment
   const int n = n0 + 64 * wn + 8 * c8;     // its first feature
-  uint4 auxv[2][4];
-  if constexpr (EPI == kEpiDGelu) {
+  // (the 256-token tile has no registers left for all of them: it loads each sub-tile's chunks
+  // at the start of that sub-tile's epilogue)
+  constexpr int UA = UM == 2 ? 2 : 1;
+  uint4 auxv[UA][4];
+  auto load_aux = [&](int ua, int u) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int m = m0 + 64 * wm + 32 * u + 8 * it + (lane >> 3);
-        auxv[u][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + AL::orow(a, m) * a.ldaux + n)
-                                           : uint4{0, 0, 0, 0};
-      }
+    for (int it = 0; it < 4; ++it) {
+      const int m = m0 + WT * wm + 32 * u + 8 * it + (lane >> 3);
+      auxv[ua][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + AL::orow(a, m) * a.ldaux + n)
+                                          : uint4{0, 0, 0, 0};
+    }
+  };
+  if constexpr (EPI == kEpiDGelu && UM == 2) {
+    load_aux(0, 0);
+    load_aux(1, 1);
   }
-  f32x16 acc[2][2];   // [feature sub-tile t][token sub-tile u]
+  f32x16 acc[2][UM];   // [feature sub-tile t][token sub-tile u]
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[t][u] = zero16();
+    for (int u = 0; u < UM; ++u) acc[t][u] = zero16();
 
   auto compute = [&](const char* ima, const char* imb) {
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const bf16x8 b0 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + r, s, h);
       const bf16x8 b1 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + 32 + r, s, h);
-      const bf16x8 a0 = Img<__bf16, BK>::rowfrag(ima, 64 * wm + r, s, h);
-      const bf16x8 a1 = Img<__bf16, BK>::rowfrag(ima, 64 * wm + 32 + r, s, h);
-      acc[0][0] = MF<__bf16>::mma(b0, a0, acc[0][0]);
-      acc[0][1] = MF<__bf16>::mma(b0, a1, acc[0][1]);
-      acc[1][0] = MF<__bf16>::mma(b1, a0, acc[1][0]);
-      acc[1][1] = MF<__bf16>::mma(b1, a1, acc[1][1]);
+      bf16x8 av[UM];
+#pragma unroll
+      for (int u = 0; u < UM; ++u) av[u] = Img<__bf16, BK>::rowfrag(ima, WT * wm + 32 * u + r, s, h);
+#pragma unroll
+      for (int u = 0; u < UM; ++u) {
+        acc[0][u] = MF<__bf16>::mma(b0, av[u], acc[0][u]);
+        acc[1][u] = MF<__bf16>::mma(b1, av[u], acc[1][u]);
+      }
     }
   };
   as[0].write(smem);
-  bs[0].write(smem + IMG);
+  bs[0].write(smem + IMGA);
   __syncthreads();
   int st = 0;
   for (; st + 2 <= nst; st += 2) {
 #pragma unroll
     for (int bsel = 0; bsel < 2; ++bsel) {
-      const char* ima = smem + bsel * 2 * IMG;
-      char* nxt = smem + (bsel ^ 1) * 2 * IMG;
+      const char* ima = smem + bsel * BUF;
+      char* nxt = smem + (bsel ^ 1) * BUF;
       // register set bsel went to LDS at the end of the previous stage: refill it (stage + 2)
       as[bsel].load(a, st + bsel + 2);
       bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (BK * 2));
-      compute(ima, ima + IMG);
+      compute(ima, ima + IMGA);
       as[bsel ^ 1].write(nxt);
-      bs[bsel ^ 1].write(nxt + IMG);
+      bs[bsel ^ 1].write(nxt + IMGA);
       __syncthreads();
     }
   }
   if (st < nst) {   // odd stage count: the last stage sits in buffer 0
-    compute(smem, smem + IMG);
+    compute(smem, smem + IMGA);
     __syncthreads();   // every wave done with buffer 0 before the epilogue reuses it as scratch
   }
 
@@ -236,16 +260,16 @@ __global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ?
         const int n = nb + 32 * t + 8 * g + 4 * h;
         const f32x4 bv = (n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[t][0][4 * g + e] += bv[e];
-          acc[t][1][4 * g + e] += bv[e];
-        }
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int u = 0; u < UM; ++u) acc[t][u][4 * g + e] += bv[e];
       }
   }
   char* scratch = smem + w * (32 * 64 * 2);   // 4 KiB per wave; the stage buffers are free now
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < UM; ++u) {
+    if constexpr (EPI == kEpiDGelu && UM != 2) load_aux(0, u);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -258,7 +282,7 @@ __global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ?
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = 8 * it + (lane >> 3);
-      const int m = m0 + 64 * wm + 32 * u + rr;
+      const int m = m0 + WT * wm + 32 * u + rr;
       const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * 128 + 16 * (c8 ^ swz<64>(rr)));
       if (m < a.M && n < a.N) {
         const long long orow = AL::orow(a, m);
@@ -269,7 +293,7 @@ __global__ __launch_bounds__(256, NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ?
           const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
           *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;
         } else {
-          const uint4 hv = auxv[u][it];
+          const uint4 hv = auxv[UM == 2 ? u : 0][it];
           const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
                            dgelu_bf2(raw.w, hv.w)};
           *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;

@@ -880,13 +880,16 @@ def patch_embed_ok(images: torch.Tensor, w: torch.Tensor, patch: Tuple[int, int]
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 
 
-# sae_gemm_nt vs the library GEMM at the training shapes (tools/gemm_probe.py,
-# profiles/r01_gemm_probe_v11.txt, profiles/r02_gemm_probe_pin_ab.txt): the HIP kernel wins for
-# reduction depths <= 384 (DeiT-S QKV forward 35 vs 78 us, output projection 16 vs 24 us) and
-# ties or wins on the narrow (384-feature) input gradients up to K = 1536 (DeiT-S / CaiT QKV dX
-# 33.7 vs 35.6 us, FF Dense_0 dX 43.1 vs 43.0); the library keeps the deep, wide ViT-B shapes
-# (K 768 .. 3072 into 768 .. 3072 features: 780 vs 840-1090 TF/s); the FF block always fuses its
-# GELU / GELU' into sae_gemm_nt.
+# sae_gemm_nt vs the library GEMM at the training shapes (tools/gemm_probe.py, tools/nt_probe.py;
+# profiles/r01_gemm_probe_v11.txt, r02_gemm_probe_pin_ab.txt, r03n_nt_probe.txt): the HIP kernel
+# wins for reduction depths <= 384 (DeiT-S QKV forward 35 vs 78 us, output projection 16 vs 24 us)
+# and ties or wins on the narrow (384-feature) input gradients up to K = 1536 (DeiT-S / CaiT QKV
+# dX).  The ViT-B@384 projections stay on the library: in isolation sae_gemm_nt matches it at
+# K = 768 (750-800 TF/s), but in the step (B 32: 870 128 x 128 tiles for the 768-feature
+# outputs, 1.7 rounds over the CUs) the library's 256 x 256 stream-K kernels are faster --
+# same-box A/B (profiles/r03o_vitb_route_ab.txt): every GEMM on sae_gemm_nt 19.0 ms/step, K <= 768
+# on it 18.0, this split 17.8.  GEMM_NT_ALL = True routes everything to sae_gemm_nt (A/B runs).
+GEMM_NT_ALL = False
 GEMM_NT_MAX_K = 512
 GEMM_NT_NARROW_N = 384
 GEMM_NT_NARROW_MAX_K = 1536
@@ -894,7 +897,7 @@ GEMM_NT_NARROW_MAX_K = 1536
 
 def use_gemm_nt(K: int, N: int) -> bool:
     """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt."""
-    return K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
+    return GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
 
 
 def _nt_ok(a2: torch.Tensor, N: int) -> bool:

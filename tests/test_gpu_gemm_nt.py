@@ -47,7 +47,8 @@ def test_gemm_nt_plain(dev, M, K, N, bias):
     assert _rel(c, ref) <= 1e-2
 
 
-@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136)])
+# (6000, 768, 3072): the ViT-B FF shape on the 256-token tile (>= 512 tiles), ragged last tile
+@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136), (6000, 768, 3072)])
 def test_gemm_nt_gelu(dev, M, K, N):
     import sae_vision_amd.ops as ops
     a, bt, b = _inputs(dev, M, K, N, 11)
@@ -60,7 +61,8 @@ def test_gemm_nt_gelu(dev, M, K, N):
     assert float((y.float() - ref_y).abs().max()) <= 2 ** -7 * float(ref_y.abs().max())
 
 
-@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136)])
+# (6000, 768, 3072): the ViT-B FF shape on the 256-token tile (>= 512 tiles), ragged last tile
+@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (130, 128, 136), (6000, 768, 3072)])
 def test_gemm_nt_dgelu(dev, M, K, N):
     import sae_vision_amd.ops as ops
     a, bt, _ = _inputs(dev, M, K, N, 12)
