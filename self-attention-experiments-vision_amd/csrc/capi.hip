@@ -529,7 +529,8 @@ static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hip
 // one sae_gemm_nt launch: TM x 128 tiles, two LDS stage buffers of BK-deep A and B images
 template <int EPI, class AL>
 static int nt_launch(const NtArgs& g, long long grid, hipStream_t st) {
-  const size_t lds = 2 * (NtRows<AL>::value + kNtT) * NtDepth<AL>::value * 2;
+  size_t lds = 2 * (NtRows<AL>::value + kNtT) * NtDepth<AL>::value * 2;
+  if constexpr (NtIsDma<AL>::value) lds = (size_t)AL::kNB * 2 * kNtT * 32 * 2;
   if (int rc = lds_attr((const void*)gemm_nt_kernel<EPI, AL>, lds)) return rc;
   hipLaunchKernelGGL((gemm_nt_kernel<EPI, AL>), dim3((unsigned)grid), dim3(256), lds, st, g);
   return 0;
@@ -1083,9 +1084,25 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   // tools/nt_probe.py at M 36928 K 768 N 3072: GELU 512 -> 634, GELU' 548 -> 609 TF/s) when that
   // still gives >= 2 tiles per CU; 128 otherwise (plain GEMMs: no gain, profiles/r03n_nt_probe.txt)
   const long long tn = (N + kNtT - 1) / kNtT;
+  const long long grid128 = (long long)((M + kNtT - 1) / kNtT) * tn;
+  (void)grid128;
   bool tall = epilogue != SAE_EPI_NONE && K >= 768 && (long long)((M + 255) / 256) * tn >= 512;
 #ifdef SAE_DEV_KNOBS
-  if (int v = dev_knob("SAE_NT_VARIANT")) tall = v == 2;
+  const int ntv = dev_knob("SAE_NT_VARIANT");
+  if (ntv) tall = ntv == 2;
+  if (ntv == 3 || ntv == 4) {   // LDS-DMA staging, 3 / 4 stage buffers
+    int rc;
+    if (ntv == 3)
+      rc = epilogue == SAE_EPI_NONE ? nt_launch<kEpiNone, NtDmaA<3>>(g, grid128, st)
+           : epilogue == SAE_EPI_GELU ? nt_launch<kEpiGelu, NtDmaA<3>>(g, grid128, st)
+                                      : nt_launch<kEpiDGelu, NtDmaA<3>>(g, grid128, st);
+    else
+      rc = epilogue == SAE_EPI_NONE ? nt_launch<kEpiNone, NtDmaA<4>>(g, grid128, st)
+           : epilogue == SAE_EPI_GELU ? nt_launch<kEpiGelu, NtDmaA<4>>(g, grid128, st)
+                                      : nt_launch<kEpiDGelu, NtDmaA<4>>(g, grid128, st);
+    if (rc) return rc;
+    return check_launch("gemm_nt");
+  }
 #endif
   const int TM = tall ? 256 : kNtT;
   const long long grid = (long long)((M + TM - 1) / TM) * tn;

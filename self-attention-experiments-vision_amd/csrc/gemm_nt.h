@@ -134,39 +134,31 @@ template <int BK, int ROWS = 128> struct NtRowAT {
 };
 using NtRowA = NtRowAT<kNtK>;
 
+// marker loader: A and B staged by LDS-DMA through NB stage buffers (32-deep stages, 128 rows)
+template <int NB> struct NtDmaA {
+  static constexpr int kBK = 32;
+  static constexpr int kNB = NB;
+  static __device__ __forceinline__ long long orow(const NtArgs&, int m) { return m; }
+};
+
 template <class AL> struct NtDepth { static constexpr int value = kNtK; };
 template <int BK, int ROWS> struct NtDepth<NtRowAT<BK, ROWS>> { static constexpr int value = BK; };
+template <int NB> struct NtDepth<NtDmaA<NB>> { static constexpr int value = 32; };
+template <class AL> struct NtIsDma { static constexpr bool value = false; };
+template <int NB> struct NtIsDma<NtDmaA<NB>> { static constexpr bool value = true; };
 template <class AL> struct NtRows { static constexpr int value = kNtT; };
 template <int BK, int ROWS> struct NtRows<NtRowAT<BK, ROWS>> { static constexpr int value = ROWS; };
 
-// Tiles: TM (128 or 256) tokens x 128 features per workgroup, each wave TM / 2 tokens x 64
-// features (UM = TM / 64 token sub-tiles of 32).  The 256-token tile reads 6 fragments from LDS
-// per 8 MFMAs instead of 4 per 4 (43 vs 32 flop per LDS byte: the 128-token tile saturates LDS
-// bandwidth before the MFMA pipe) and fetches the weight once per 256 tokens; it runs 32-deep
-// stages so that the two staged register sets still fit beside the 128 accumulator registers.
-template <int EPI, class AL>
-constexpr int nt_min_blocks() {
-  return NtRows<AL>::value == 256 ? 2 : NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ? 3 : 4) : 2;
-}
-
-template <int EPI, class AL = NtRowA>
-__global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kernel(NtArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BK = NtDepth<AL>::value;   // K per stage
-  constexpr int TM = NtRows<AL>::value;    // tokens per tile
-  constexpr int UM = TM / 64;              // 32-token sub-tiles per wave
-  constexpr int IMGA = TM * BK * 2;        // A image (16 KiB at 128 x 64)
-  constexpr int IMG = kNtT * BK * 2;       // B image
-  constexpr int BUF = IMGA + IMG;
-  const int tn = (a.N + kNtT - 1) / kNtT;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = bid / tn, nt = bid % tn;
-  const int m0 = mt * TM, n0 = nt * kNtT;
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w & 1, wn = w >> 1;   // this wave's TM / 2 (tokens) x 64 (features) quarter
-  constexpr int WT = TM / 2;
-
+// Main loop, operands staged global -> registers -> LDS: two LDS buffers, two register sets in
+// flight.  Straight-line staging (no data-dependent branches around the loads and LDS writes):
+// the loads of stages st + 2 and the LDS writes of stage st + 1 are issued unconditionally -- past
+// the end they read zeros (descriptor range check) or unused bytes into a buffer nobody reads
+// again -- so the waitcnt pass can prove each register set's loads retired and keeps two stages
+// in flight (with conditional loads it waited vmcnt(0) before every reload).
+template <class AL, int BK, int TM, class Pre, class Compute>
+__device__ __forceinline__ void nt_loop_regs(const NtArgs& a, int m0, int n0, int tid, char* smem, Pre&& preload,
+                                             Compute&& compute) {
+  constexpr int IMGA = TM * BK * 2, IMG = kNtT * BK * 2, BUF = IMGA + IMG;
   // rows past N read zero through the descriptor's range check
   const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
   AL as[2];
@@ -177,56 +169,11 @@ __global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kerne
     bs[q].init(tid, a.ldb);
   }
   const int nst = a.K / BK;
-  // Straight-line staging (no data-dependent branches around the loads and LDS writes): the
-  // loads of stages st + 2 and the LDS writes of stage st + 1 are issued unconditionally --
-  // past the end they read zeros (descriptor range check) or unused bytes into a buffer nobody
-  // reads again -- so the waitcnt pass can prove each register set's loads retired and keeps two
-  // stages in flight (with conditional loads it waited vmcnt(0) before every reload).
   as[0].load(a, 0);
   bs[0].load(rb, 0);
   as[1].load(a, 1);
   bs[1].load(rb, BK * 2);
-  // kEpiDGelu: this lane's eight aux chunks (the epilogue's row groups) are loaded before the
-  // main loop, so their HBM traffic overlaps the MFMAs instead of following them
-  const int c8 = lane & 7;                 // 16-byte chunk of an epilogue row segment
-  const int n = n0 + 64 * wn + 8 * c8;     // its first feature
-  // (the 256-token tile has no registers left for all of them: it loads each sub-tile's chunks
-  // at the start of that sub-tile's epilogue)
-  constexpr int UA = UM == 2 ? 2 : 1;
-  uint4 auxv[UA][4];
-  auto load_aux = [&](int ua, int u) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int m = m0 + WT * wm + 32 * u + 8 * it + (lane >> 3);
-      auxv[ua][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + AL::orow(a, m) * a.ldaux + n)
-                                          : uint4{0, 0, 0, 0};
-    }
-  };
-  if constexpr (EPI == kEpiDGelu && UM == 2) {
-    load_aux(0, 0);
-    load_aux(1, 1);
-  }
-  f32x16 acc[2][UM];   // [feature sub-tile t][token sub-tile u]
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < UM; ++u) acc[t][u] = zero16();
-
-  auto compute = [&](const char* ima, const char* imb) {
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const bf16x8 b0 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + r, s, h);
-      const bf16x8 b1 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + 32 + r, s, h);
-      bf16x8 av[UM];
-#pragma unroll
-      for (int u = 0; u < UM; ++u) av[u] = Img<__bf16, BK>::rowfrag(ima, WT * wm + 32 * u + r, s, h);
-#pragma unroll
-      for (int u = 0; u < UM; ++u) {
-        acc[0][u] = MF<__bf16>::mma(b0, av[u], acc[0][u]);
-        acc[1][u] = MF<__bf16>::mma(b1, av[u], acc[1][u]);
-      }
-    }
-  };
+  preload();
   as[0].write(smem);
   bs[0].write(smem + IMGA);
   __syncthreads();
@@ -249,6 +196,187 @@ __global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kerne
     compute(smem, smem + IMGA);
     __syncthreads();   // every wave done with buffer 0 before the epilogue reuses it as scratch
   }
+}
+
+// One 16-byte-per-lane LDS-DMA piece (1 KiB at the wave-uniform LDS byte address `lds`: lane L's
+// 16 bytes land at lds + 16 L).  Inline asm on purpose: through the builtin, hipcc cannot tell the
+// DMA's LDS bytes from the ones a later ds_read reads and puts an s_waitcnt vmcnt(0) in front of
+// it, which drains every stage in flight.  The waits are counted by hand instead (nt_loop_dma).
+// M0 is compiler-reserved: saved and restored inside the statement (s_nop 4 for a descriptor
+// just written by SALU, s_nop 0 after the M0 write).
+typedef __attribute__((ext_vector_type(4))) unsigned nt_u32x4;
+__device__ __forceinline__ void nt_dma16(nt_u32x4 rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds)
+      : "memory");
+}
+
+// the four words of row_rsrc's descriptor (common.h), for the inline-asm DMA
+template <typename T>
+__device__ __forceinline__ nt_u32x4 nt_rsrc_words(const T* base, int nrows, long long rs) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  nt_u32x4 w;
+  w[0] = __builtin_amdgcn_readfirstlane((unsigned)p);
+  w[1] = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32)) & 0xffffu;   // stride 0
+  w[2] = __builtin_amdgcn_readfirstlane((unsigned)((long long)nrows * rs * sizeof(T)));
+  w[3] = 0x00020000u;
+  return w;
+}
+
+// s_waitcnt vmcnt(N) + s_barrier as one statement: the "memory" clobber keeps the compiler from
+// moving LDS accesses across it (the builtin barrier is not a memory operation to the compiler)
+template <int N>
+__device__ __forceinline__ void nt_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// Main loop, operands staged by LDS-DMA (no VGPR round trip, no ds_write): 128 x 32 A and B
+// images per stage (8 KiB each = 8 one-KiB pieces, XOR-swizzled like Img<bf16, 32>: lane L of a
+// piece fetches the global chunk (L & 3) ^ swz(row) so the image holds chunk c at c ^ swz(row)),
+// NB stage buffers, NB - 1 stages in flight.  Each wave issues 4 pieces per stage; at the top of
+// stage st it waits until only the (NB - 2) newer stages' pieces are outstanding, and the barrier
+// makes every wave's pieces of stage st visible and frees the buffer the next issue overwrites
+// (computed at st - 1).  Stages past K are issued anyway (rows read zero or bytes nobody reads)
+// so that the count stays uniform.
+template <int NB, class Pre, class Compute>
+__device__ __forceinline__ void nt_loop_dma(const NtArgs& a, int m0, int n0, int w, int lane, char* smem,
+                                            Pre&& preload, Compute&& compute) {
+  constexpr int BK = 32, IMG = kNtT * BK * 2, BUF = 2 * IMG;
+  const nt_u32x4 ra = nt_rsrc_words(a.a + (long long)m0 * a.lda, min(kNtT, a.M - m0), a.lda);
+  const nt_u32x4 rb = nt_rsrc_words(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
+  const unsigned lbase = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+  // this wave's pieces: A pieces w and w + 4, B pieces w and w + 4 (16 rows of 64 bytes each)
+  unsigned goa[2], gob[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (w + 4 * i) + (lane >> 2);
+    const int c = (lane & 3) ^ swz<BK>(row);
+    goa[i] = (unsigned)(((long long)row * a.lda + 8 * c) * 2);
+    gob[i] = (unsigned)(((long long)row * a.ldb + 8 * c) * 2);
+  }
+  auto issue = [&](int st, int buf) {
+    const unsigned ko = (unsigned)st * (BK * 2);
+    const unsigned lb = lbase + (unsigned)(buf * BUF) + (unsigned)(w * 1024);
+    // the stage's four pieces in one statement: one M0 save / restore, one descriptor settle
+    unsigned keep;
+    asm volatile(
+        "s_nop 4\n\t"
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %7\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %5, 0 offen lds\n\t"
+        "s_add_u32 m0, %7, 4096\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %5, 0 offen lds\n\t"
+        "s_add_u32 m0, %7, 8192\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
+        "s_add_u32 m0, %7, 12288\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(goa[0] + ko), "v"(goa[1] + ko), "v"(gob[0] + ko), "v"(gob[1] + ko), "s"(ra), "s"(rb), "s"(lb)
+        : "memory", "scc");
+  };
+  static_assert(IMG == 8192, "piece layout: A pieces w, w + 4 at +0 / +4 KiB, B at +8 / +12 KiB");
+  const int nst = a.K / BK;
+#pragma unroll
+  for (int q = 0; q < NB - 1; ++q) issue(q, q);
+  preload();
+  int cur = 0, nxt = NB - 1;
+  for (int st = 0; st < nst; ++st) {
+    nt_wait_barrier<4 * (NB - 2)>();
+    issue(st + NB - 1, nxt);
+    compute(smem + cur * BUF, smem + cur * BUF + IMG);
+    cur = cur + 1 == NB ? 0 : cur + 1;
+    nxt = nxt + 1 == NB ? 0 : nxt + 1;
+  }
+  nt_wait_barrier<0>();   // every piece landed and every wave done before the epilogue's scratch
+}
+
+// Tiles: TM (128 or 256) tokens x 128 features per workgroup, each wave TM / 2 tokens x 64
+// features (UM = TM / 64 token sub-tiles of 32).  The 256-token tile reads 6 fragments from LDS
+// per 8 MFMAs instead of 4 per 4 (43 vs 32 flop per LDS byte: the 128-token tile saturates LDS
+// bandwidth before the MFMA pipe) and fetches the weight once per 256 tokens; it runs 32-deep
+// stages so that the two staged register sets still fit beside the 128 accumulator registers.
+template <int EPI, class AL>
+constexpr int nt_min_blocks() {
+  if constexpr (NtIsDma<AL>::value) return AL::kNB <= 3 ? 3 : 2;
+  return NtRows<AL>::value == 256 ? 2 : NtDepth<AL>::value == 32 ? (EPI == kEpiDGelu ? 3 : 4) : 2;
+}
+
+template <int EPI, class AL = NtRowA>
+__global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kernel(NtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BK = NtDepth<AL>::value;   // K per stage
+  constexpr int TM = NtRows<AL>::value;    // tokens per tile
+  constexpr int UM = TM / 64;              // 32-token sub-tiles per wave
+  const int tn = (a.N + kNtT - 1) / kNtT;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tn, nt = bid % tn;
+  const int m0 = mt * TM, n0 = nt * kNtT;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;   // this wave's TM / 2 (tokens) x 64 (features) quarter
+  constexpr int WT = TM / 2;
+
+  // kEpiDGelu: this lane's eight aux chunks (the epilogue's row groups) are loaded before the
+  // main loop, so their HBM traffic overlaps the MFMAs instead of following them
+  const int c8 = lane & 7;                 // 16-byte chunk of an epilogue row segment
+  const int n = n0 + 64 * wn + 8 * c8;     // its first feature
+  // (the 256-token tile has no registers left for all of them: it loads each sub-tile's chunks
+  // at the start of that sub-tile's epilogue)
+  constexpr int UA = UM == 2 ? 2 : 1;
+  uint4 auxv[UA][4];
+  auto load_aux = [&](int ua, int u) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int m = m0 + WT * wm + 32 * u + 8 * it + (lane >> 3);
+      auxv[ua][it] = (m < a.M && n < a.N) ? *reinterpret_cast<const uint4*>(a.aux + AL::orow(a, m) * a.ldaux + n)
+                                          : uint4{0, 0, 0, 0};
+    }
+  };
+  auto preload = [&]() {
+    if constexpr (EPI == kEpiDGelu && UM == 2) {
+      load_aux(0, 0);
+      load_aux(1, 1);
+    }
+  };
+  f32x16 acc[2][UM];   // [feature sub-tile t][token sub-tile u]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < UM; ++u) acc[t][u] = zero16();
+
+  auto compute = [&](const char* ima, const char* imb) {
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const bf16x8 b0 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + r, s, h);
+      const bf16x8 b1 = Img<__bf16, BK>::rowfrag(imb, 64 * wn + 32 + r, s, h);
+      bf16x8 av[UM];
+#pragma unroll
+      for (int u = 0; u < UM; ++u) av[u] = Img<__bf16, BK>::rowfrag(ima, WT * wm + 32 * u + r, s, h);
+#pragma unroll
+      for (int u = 0; u < UM; ++u) {
+        acc[0][u] = MF<__bf16>::mma(b0, av[u], acc[0][u]);
+        acc[1][u] = MF<__bf16>::mma(b1, av[u], acc[1][u]);
+      }
+    }
+  };
+  if constexpr (NtIsDma<AL>::value)
+    nt_loop_dma<AL::kNB>(a, m0, n0, w, lane, smem, preload, compute);
+  else
+    nt_loop_regs<AL, BK, TM>(a, m0, n0, tid, smem, preload, compute);
 
   // ---- epilogue: accumulator row = feature nb + 32t + row_of(reg, h), column = token (lane)
   const int nb = n0 + 64 * wn;

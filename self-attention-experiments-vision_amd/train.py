@@ -531,6 +531,28 @@ class TrainStep:
             self._g = self._g_opt = None
             torch.cuda.synchronize()
 
+    def close(self):
+        """Release the captured graphs and the optimizer's persistent bf16 copies.  With a process
+        group, call it BEFORE destroy_process_group: a graph whose capture holds RCCL collectives
+        keeps communicator resources that its destruction releases, so it must not outlive the
+        communicator (left to the garbage collector, it was destroyed at an arbitrary later point)."""
+        if self._g is not None or self._g_opt is not None:
+            torch.cuda.synchronize()
+        self._g = self._g_opt = None
+        if self.collective == "overlap":
+            from . import ops
+            ops.set_sink_listener(None)
+        if isinstance(self.opt, FusedAdamW):
+            self.opt.close()
+
+    def input_buffers(self):
+        """(images, labels): the captured graph's static input buffers, once the first call has
+        captured it (None otherwise).  A loader that writes each batch into them saves the copy a
+        call with other tensors makes before the replay."""
+        if self._g is None:
+            return None
+        return self._images, self._labels
+
     def __call__(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         if not self.graph:
             return self._eager(images, labels)

@@ -149,50 +149,19 @@ def test_grad_sink_follows_param_grad(dev):
 
 @pytest.mark.parametrize("model", ["deit_ti_patch16", "cait"])
 def test_world1_rccl_overlapped_step(dev, model):
-    """The multi-rank step's collective path on one GPU: a one-rank RCCL group (backend nccl), the
-    bucket all-reduces launched from inside the backward on the communication stream and captured
-    with the rest of the step in ONE HIP graph (train.py "overlap").  A one-rank SUM is the
-    identity, so losses and parameters must equal the no-collective graph step's bit for bit; the
-    buckets must all have been launched, the first before the backward finished."""
+    """The multi-rank step's collective path on one GPU (tests/world1_rccl_case.py): a one-rank
+    RCCL group, the bucket all-reduces launched from inside the backward on the communication
+    stream and captured with the rest of the step in ONE HIP graph; losses and parameters equal to
+    the no-collective graph step's bit for bit.  Run in a child process: the RCCL communicator and
+    the graphs that captured its collectives live and die there (the child tears them down in the
+    right order) and its stderr is reported if it fails."""
+    import subprocess
+    import sys
     import os
-    import socket
-    import torch.distributed as dist
-    from sae_vision_amd import cait, train, vit
-    torch.manual_seed(0)
-    if model == "cait":
-        m_a = cait.create_cait("cait_xxs_24", 1000, torch.bfloat16, stoch_depth=False, device=dev)
-    else:
-        m_a = vit.create_model(model, 1000, torch.bfloat16, device=dev)
-    m_b = copy.deepcopy(m_a)
-    s_a = train.TrainStep(m_a, global_batch=8, device=dev, graph=True)
-    assert s_a.collective == "none"
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1)
-    try:
-        s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=True, bucket_cap_mb=4.0)
-        assert s_b.collective == "overlap" and len(s_b._buckets) > 1
-        order = []
-        orig = s_b._launch_bucket
-        s_b._launch_bucket = lambda bi: (order.append((bi, len(s_b._ready))), orig(bi))[1]
-        g = torch.Generator(device=dev).manual_seed(3)
-        data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
-                 torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
-        la = [float(s_a(x, y)) for x, y in data]
-        lb = [float(s_b(x, y)) for x, y in data]
-        assert s_b._g is not None and s_b._g_opt is None and s_b.graph   # one graph, collectives inside
-        nb = len(s_b._buckets)
-        assert sorted(bi for bi, _ in order[-nb:]) == list(range(nb))     # the captured backward's launches
-        assert order[-nb][1] < len(s_b._params)                            # the first before the last gradient
-        assert la == lb, (la, lb)
-        for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
-            assert torch.equal(pa, pb), n
-    finally:
-        dist.destroy_process_group()
-        from sae_vision_amd import ops
-        ops.set_sink_listener(None)
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "world1_rccl_case.py")
+    r = subprocess.run([sys.executable, "-u", script, model], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "WORLD1_OK" in r.stdout, \
+        f"rc {r.returncode}\nstdout:\n{r.stdout[-2000:]}\nstderr:\n{r.stderr[-4000:]}"
 
 
 def test_fused_adamw_cast_copies(dev):
