@@ -140,3 +140,34 @@ def test_patch_embed_validation():
         assert lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(d)) == 0
     ok = L.SaePatchDesc(128, 224, 224, 3, 16, 16, 384, L.SAE_LAYOUT_HWCN, L.SAE_DTYPE_F32)
     assert lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(ok)) > 0
+
+
+def test_adamw_cast_plan_tiles_and_refusals():
+    """sae_adamw_cast_plan (host only, no GPU): 64 x 64 tiles per Dense kernel with the column
+    offset / leading dimensions carried into each tile, the capacity check, and SAE_EUNSUPPORTED
+    for shapes or buffers the vector tile path does not take."""
+    import sae_vision_amd._lib as L
+    lib = L.load()
+    base = 1 << 20   # fake 16-byte-aligned device addresses: the planner only does arithmetic
+
+    def plan(K, N, col0=0, ld16=None, off=0, cap=64):
+        arr = lambda t, *v: (t * len(v))(*v)
+        P, G, M, V = (arr(ctypes.c_void_p, base + 0x1000 * i + off) for i in range(4))
+        W16, WT = arr(ctypes.c_void_p, base + 0x100000), arr(ctypes.c_void_p, base + 0x200000)
+        tiles = (L.AdamwCastTile * cap)()
+        n = ctypes.c_int64(0)
+        rc = lib.sae_adamw_cast_plan(1, P, G, M, V, arr(ctypes.c_int32, K), arr(ctypes.c_int32, N), W16,
+                                     arr(ctypes.c_int32, ld16 if ld16 is not None else col0 + N), WT,
+                                     arr(ctypes.c_int32, K), arr(ctypes.c_int32, col0), tiles, cap, ctypes.byref(n))
+        return rc, n.value, tiles
+
+    rc, n, t = plan(68, 100, col0=36, ld16=136)
+    assert rc == L.SAE_OK and n == 4
+    assert sorted((x.k0, x.n0) for x in t[:4]) == [(0, 0), (0, 64), (64, 0), (64, 64)]
+    assert all(x.K == 68 and x.N == 100 and x.col0 == 36 and x.ld16 == 136 and x.ldT == 68 for x in t[:4])
+    rc, n, _ = plan(384, 1152, cap=10)            # 6 x 18 tiles > capacity: counted, refused
+    assert rc == L.SAE_EINVAL and n == 108
+    assert plan(66, 100)[0] == L.SAE_EUNSUPPORTED            # K not a multiple of 4
+    assert plan(68, 100, col0=2, ld16=104)[0] == L.SAE_EUNSUPPORTED   # column offset
+    assert plan(68, 100, off=8)[0] == L.SAE_EUNSUPPORTED     # fp32 buffers not 16-byte aligned
+    assert plan(68, 100, col0=8, ld16=100)[0] == L.SAE_EINVAL          # ld16 < col0 + N
