@@ -255,8 +255,9 @@ int sae_layernorm_fwd(void* stream, int32_t M, int32_t C, const float* x, const 
                       float* xout, const float* gamma, const float* beta, void* y, float* mean,
                       float* rstd, float eps);
 /* CaiT form (layerscale.py:21-23, stochastic_depth.py:19-28 folded into the residual add):
-     xout = x + delta * layerscale[c] * rowscale[row / rows_per_sample]   (rowscale may be NULL)
-   layerscale fp32 [C] (16-byte aligned), rowscale fp32 [M / rows_per_sample]. */
+     xout = x + delta * bf16(layerscale[c]) * rowscale[row / rows_per_sample]   (rowscale may be NULL)
+   layerscale fp32 [C] (16-byte aligned; the parameter as stored -- the kernels round it to bf16,
+   the compute-dtype cast of layerscale.py:22), rowscale fp32 [M / rows_per_sample]. */
 int sae_layernorm_fwd_scaled(void* stream, int32_t M, int32_t C, const float* x, const void* delta,
                              float* xout, const float* gamma, const float* beta, void* y,
                              float* mean, float* rstd, float eps, const float* layerscale,

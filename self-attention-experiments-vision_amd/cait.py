@@ -72,11 +72,31 @@ def scaled_branch(x: torch.Tensor, ls: LayerScaleBlock, sd: StochasticDepthBlock
     return x.to(dtype) * f
 
 
+# the factors of every stochastic-depth block of one training forward, drawn together
+# (CaiT.forward): one uniform draw and two elementwise passes instead of four launches per block
+_SD_DRAW = None
+
+
+class _SDDraw:
+    def __init__(self, rows: torch.Tensor, index):
+        self.rows, self.index = rows, index
+
+
+def draw_stochastic_depth(sds, keep: torch.Tensor, batch: int, device) -> "_SDDraw":
+    """rows[i] = floor(keep_i + U[0,1)) / keep_i for every block i of ``sds`` (keep [n, 1] on the
+    device): the same per-sample factor as sample_scale, for all blocks in one draw."""
+    u = torch.rand((len(sds), batch), device=device, dtype=torch.float32)
+    return _SDDraw(torch.floor(keep + u) / keep, {id(sd): i for i, sd in enumerate(sds)})
+
+
 def sample_scale(batch: int, sd: StochasticDepthBlock, is_training: bool, device):
     """Per-sample stochastic-depth factor floor(keep + U[0,1)) / keep (stochastic_depth.py:19-28),
-    or None when the block is the identity."""
+    or None when the block is the identity; from the forward's joint draw when there is one."""
     if not is_training or sd.drop_rate == 0.0:
         return None
+    d = _SD_DRAW
+    if d is not None and id(sd) in d.index and d.rows.shape[1] == batch:
+        return d.rows[d.index[id(sd)]]
     keep = 1.0 - sd.drop_rate
     return torch.floor(keep + torch.rand((batch,), device=device, dtype=torch.float32)) / keep
 
@@ -213,14 +233,48 @@ class CaiT(nn.Module):
         self.LayerNorm_0 = LayerNorm(embed_dim, device)
         self.Dense_0 = Dense(embed_dim, num_classes, zero_init=True, device=device)
 
+    def cast_groups(self):
+        """The Dense kernels whose bf16 copies the optimizer may keep (FusedAdamW ``cast_groups``):
+        the trunk's column-block groups (when the trunk computes in bf16), the patch embedding and
+        the head and the class-attention blocks' projections / FF (when the model does)."""
+        groups = []
+        blocks = [getattr(self.Encoder_0, f"EncoderBlock_{i}") for i in range(self.Encoder_0.num_layers)]
+        if blocks and blocks[0].dtype == torch.bfloat16:
+            groups += encoder_weight_groups(blocks)
+        if self.dtype == torch.bfloat16:
+            groups += [[self.PatchEmbedBlock_0.Dense_0.kernel], [self.Dense_0.kernel]]
+            for i in range(self.num_layers_token_only):
+                ca = getattr(self, f"CAEncoderBlock_{i}")
+                groups += ca.ClassSelfAttentionBlock_0.cross_weight_groups()
+                groups += [[ca.FFBlock_0.Dense_0.kernel], [ca.FFBlock_0.Dense_1.kernel]]
+        return groups or None
+
+    def _sd_blocks(self, device):
+        """The stochastic-depth blocks with a non-zero rate and their keep probabilities [n, 1] on
+        the device (built once: inside a graph capture no host-to-device copy may run)."""
+        c = getattr(self, "_sd_cache", None)
+        if c is None or c[1].device != device:
+            sds = [m for m in self.modules() if isinstance(m, StochasticDepthBlock) and m.drop_rate > 0.0]
+            keep = torch.tensor([[1.0 - m.drop_rate] for m in sds], dtype=torch.float32, device=device)
+            c = self._sd_cache = (sds, keep)
+        return c
+
     def forward(self, inputs: torch.Tensor, is_training: bool, layout: str = "NHWC") -> torch.Tensor:
         """``layout`` "HWCN": ``inputs`` is the train-step feed [H, W, C, B] (train.py:80)."""
+        global _SD_DRAW
         x = patch_tokens(self.PatchEmbedBlock_0, inputs, self.patch_shape, self.dtype, layout)
         b = x.shape[0]
-        x = self.Encoder_0(x, is_training)
-        cls_token = self.cls.expand(b, 1, self.embed_dim).float()
-        for i in range(self.num_layers_token_only):
-            cls_token = getattr(self, f"CAEncoderBlock_{i}")(x, cls_token, is_training)
+        sds, keep = self._sd_blocks(x.device)
+        prev = _SD_DRAW
+        if is_training and sds:   # every block's per-sample factor in one draw
+            _SD_DRAW = draw_stochastic_depth(sds, keep, b, x.device)
+        try:
+            x = self.Encoder_0(x, is_training)
+            cls_token = self.cls.expand(b, 1, self.embed_dim).float()
+            for i in range(self.num_layers_token_only):
+                cls_token = getattr(self, f"CAEncoderBlock_{i}")(x, cls_token, is_training)
+        finally:
+            _SD_DRAW = prev
         # LayerNorm over [cls, x] then take the CLS row: LN is per token, so normalising the CLS row
         # alone is the same value (cait.py:179-183) without the 197-token pass
         cls_n = self.LayerNorm_0(cls_token[:, 0], self.dtype)

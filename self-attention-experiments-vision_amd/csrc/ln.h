@@ -34,8 +34,9 @@ struct LnArgs {
   float* dgamma;         // [C]
   float* dbeta;          // [C]
   // CaiT branch scale (layerscale.py:21-23 x stochastic_depth.py:19-28) folded into the add:
-  // x_out = x + delta * lsc[c] * rsc[row / rpb]   (lsc, rsc may be null = 1)
-  const float* lsc;      // [C] LayerScale parameter
+  // x_out = x + delta * bf16(lsc[c]) * rsc[row / rpb]   (lsc, rsc may be null = 1; the LayerScale
+  // parameter is used at the compute dtype, layerscale.py:22, rounded here as it is loaded)
+  const float* lsc;      // [C] LayerScale parameter (fp32)
   const float* rsc;      // [M / rpb] per-sample stochastic-depth factor (mask / keep)
   float* dlsc;           // [C] gradient of lsc (backward; needs delta)
   int rpb;               // rows per sample
@@ -62,6 +63,12 @@ __device__ __forceinline__ void st_bf16x4(__bf16* p, f32x4 v) {
   *reinterpret_cast<bf16x4*>(p) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
 }
 
+// fp32 -> the nearest bf16 value, as fp32 (the LayerScale parameter at the compute dtype;
+// idempotent, so a caller passing already-rounded values gets the same result)
+__device__ __forceinline__ f32x4 ln_bf16r(f32x4 v) {
+  return f32x4{(float)(__bf16)v[0], (float)(__bf16)v[1], (float)(__bf16)v[2], (float)(__bf16)v[3]};
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   const int lane = threadIdx.x & 63;
@@ -79,7 +86,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = lane + 64 * k;
-    ls[k] = (a.lsc && c < C4) ? reinterpret_cast<const f32x4*>(a.lsc)[c] : f32x4{1.f, 1.f, 1.f, 1.f};
+    ls[k] = (a.lsc && c < C4) ? ln_bf16r(reinterpret_cast<const f32x4*>(a.lsc)[c]) : f32x4{1.f, 1.f, 1.f, 1.f};
   }
   const float invC = 1.f / (float)a.C;
   for (int row = wave; row < a.M; row += nw) {
@@ -136,7 +143,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
   for (int k = 0; k < NV; ++k) {
     const int c = lane + 64 * k;
     g[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.gamma)[c] : f32x4{};
-    ls[k] = (NP == 3 && c < C4) ? reinterpret_cast<const f32x4*>(a.lsc)[c] : f32x4{1.f, 1.f, 1.f, 1.f};
+    ls[k] = (NP == 3 && c < C4) ? ln_bf16r(reinterpret_cast<const f32x4*>(a.lsc)[c]) : f32x4{1.f, 1.f, 1.f, 1.f};
     pg[k] = pb[k] = pl[k] = f32x4{};
   }
   const float invC = 1.f / (float)a.C;

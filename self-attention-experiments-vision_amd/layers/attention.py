@@ -118,6 +118,16 @@ class AttentionBlock(nn.Module):
         return [[m.kernel.reshape(C, HD) for m in (self.queries, self.keys, self.values)],
                 [self.DenseGeneral_0.kernel.reshape(HD, self._out_ch_eff)]]
 
+    def cross_weight_groups(self):
+        """The column blocks the projections use when queries and keys / values come from
+        different inputs (class / last-token attention): [queries], [keys | values], [output]."""
+        if self._in_ch is None:
+            return []
+        C, HD = self._in_ch, self.num_heads * self._head_ch_eff
+        return [[self.queries.kernel.reshape(C, HD)],
+                [m.kernel.reshape(C, HD) for m in (self.keys, self.values)],
+                [self.DenseGeneral_0.kernel.reshape(HD, self._out_ch_eff)]]
+
     # -- forward -----------------------------------------------------------------------
     def forward(self, inputs_q: torch.Tensor, inputs_kv: torch.Tensor, is_training: bool) -> torch.Tensor:
         assert inputs_q.ndim == inputs_kv.ndim == 3

@@ -296,9 +296,12 @@ def _th_fwd(q, k, v, th1, th2, scale, rope=None):
     return o, lse, th1c, th2c
 
 
-def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale, rope=None):
+def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale, rope=None, dth1=None, dth2=None):
+    """dT1 / dT2 go into ``dth1`` / ``dth2`` when given (fp32 [H, H]: the transforms' gradient
+    sinks -- the reduce kernel writes them whole), else into fresh tensors."""
     lib = L.load()
-    dth1, dth2 = torch.empty_like(th1), torch.empty_like(th2)
+    dth1 = torch.empty_like(th1) if dth1 is None else dth1
+    dth2 = torch.empty_like(th2) if dth2 is None else dth2
     d = _make_desc(q, k, v, None, scale, do, dq, dk, dv)
     ws = torch.empty(lib.sae_th_attn_bwd_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=q.device)
     tok = _TIMER.begin("th_attn_bwd") if _TIMER is not None else None
@@ -316,6 +319,17 @@ def _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, scale, rope=None):
     return dth1, dth2
 
 
+def _th_sinks(th1, th2):
+    """Gradient sinks of the two transforms (fp32 contiguous parameters only: the reduce kernel
+    writes fp32 [H, H] in place), or None each."""
+    ok = lambda t: t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
+    s1 = _sink(th1) if ok(th1) else None
+    s2 = _sink(th2) if ok(th2) else None
+    if s1 is not None and s2 is not None and s1.data_ptr() == s2.data_ptr():
+        s2 = None   # one parameter used as both transforms: autograd adds the two gradients
+    return s1, s2
+
+
 class _TalkingHeads(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, th1, th2, scale, rope):
@@ -324,6 +338,7 @@ class _TalkingHeads(torch.autograd.Function):
         ctx.save_for_backward(q, k, v, th1c, th2c, lse)
         ctx.scale, ctx.rope = scale, rope
         ctx.th_dtypes = (th1.dtype, th2.dtype)
+        ctx.sinks = _th_sinks(th1, th2)
         return o
 
     @staticmethod
@@ -332,8 +347,10 @@ class _TalkingHeads(torch.autograd.Function):
         q, k, v, th1, th2, lse = ctx.saved_tensors
         do = _grad_in(do)
         dq, dk, dv = (torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in (q, k, v))
-        dth1, dth2 = _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, ctx.scale, ctx.rope)
-        return dq, dk, dv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None, None
+        s1, s2 = ctx.sinks
+        dth1, dth2 = _th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, ctx.scale, ctx.rope, _claim(s1), _claim(s2))
+        return (dq, dk, dv, _unsunk(dth1.to(ctx.th_dtypes[0]), s1), _unsunk(dth2.to(ctx.th_dtypes[1]), s2), None,
+                None)
 
 
 class _TalkingHeadsPacked(torch.autograd.Function):
@@ -347,6 +364,7 @@ class _TalkingHeadsPacked(torch.autograd.Function):
         ctx.save_for_backward(qkv, th1c, th2c, lse)
         ctx.scale, ctx.rope = scale, rope
         ctx.th_dtypes = (th1.dtype, th2.dtype)
+        ctx.sinks = _th_sinks(th1, th2)
         return o
 
     @staticmethod
@@ -355,9 +373,10 @@ class _TalkingHeadsPacked(torch.autograd.Function):
         qkv, th1, th2, lse = ctx.saved_tensors
         do = _grad_in(do)
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        s1, s2 = ctx.sinks
         dth1, dth2 = _th_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], th1, th2, lse, do, dqkv[:, :, 0],
-                             dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.rope)
-        return dqkv, dth1.to(ctx.th_dtypes[0]), dth2.to(ctx.th_dtypes[1]), None, None
+                             dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.rope, _claim(s1), _claim(s2))
+        return dqkv, _unsunk(dth1.to(ctx.th_dtypes[0]), s1), _unsunk(dth2.to(ctx.th_dtypes[1]), s2), None, None
 
 
 def _th_rope_ok(q, k, v) -> bool:
@@ -1128,8 +1147,9 @@ class _AddLayerNormScaled(torch.autograd.Function):
         x, gamma, beta = _f32c(x, "x"), _f32c(gamma, "gamma"), _f32c(beta, "beta")
         delta_dtype = delta.dtype
         delta = _bf16c(delta)
-        # the reference casts the LayerScale parameter to the compute dtype (layerscale.py:22)
-        lsf = ls.detach().to(delta.dtype).float().contiguous()
+        # the reference casts the LayerScale parameter to the compute dtype (layerscale.py:22): the
+        # kernels round the fp32 parameter to bf16 as they load it (no cast launches here)
+        lsf = _f32c(ls.detach(), "layerscale")
         y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
         mean = torch.empty(M, dtype=torch.float32, device=x.device)
         rstd = torch.empty(M, dtype=torch.float32, device=x.device)

@@ -215,18 +215,22 @@ def test_fused_adamw_cast_copies(dev):
     assert ops._wkey([b[2]]) not in ops._PERSIST
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_train_step_persistent_casts_bitwise(dev, graph):
-    """DeiT-Ti training steps with the optimizer writing the bf16 Dense copies (no cast in the
-    forward) give the same losses and parameters, bit for bit, as steps that cast every forward."""
-    from sae_vision_amd import ops, train, vit
+@pytest.mark.parametrize("model,graph", [("deit_ti_patch16", False), ("deit_ti_patch16", True), ("cait", True)])
+def test_train_step_persistent_casts_bitwise(dev, model, graph):
+    """Training steps with the optimizer writing the bf16 Dense copies (no cast in the forward)
+    give the same losses and parameters, bit for bit, as steps that cast every forward (DeiT-Ti;
+    CaiT-XXS: trunk groups, class-attention cross projections, talking-heads transform sinks)."""
+    from sae_vision_amd import cait, ops, train, vit
     torch.manual_seed(0)
-    m_a = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
+    if model == "cait":
+        m_a = cait.create_cait("cait_xxs_24", 1000, torch.bfloat16, stoch_depth=False, device=dev)
+    else:
+        m_a = vit.create_model(model, 1000, torch.bfloat16, device=dev)
     m_b = copy.deepcopy(m_a)
     s_a = train.TrainStep(m_a, global_batch=8, device=dev, graph=graph, persistent_casts=False)
     s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=graph)
     assert not s_a.opt.cast_groups
-    assert len(s_b.opt.cast_groups) == len(m_b.cast_groups())   # every Dense kernel of DeiT-Ti
+    assert len(s_b.opt.cast_groups) == len(m_b.cast_groups())   # every group the model names
     g = torch.Generator(device=dev).manual_seed(3)
     data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
              torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
