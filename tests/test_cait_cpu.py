@@ -86,3 +86,30 @@ def test_cait_bf16_chain_tracks_fp64():
     finally:
         cait_ref._torch_rb = orig
     assert np.abs(exact - ref).max() / np.abs(ref).max() < 1e-12
+
+
+def test_joint_stochastic_depth_draw():
+    """draw_stochastic_depth: one uniform draw for every block, each row the per-sample factor
+    floor(keep_i + U) / keep_i (values 0 or 1 / keep_i, stochastic_depth.py:19-28); sample_scale
+    serves the drawn row for a registered block and draws on its own otherwise."""
+    import sae_vision_amd.cait as cait
+    sds = [cait.StochasticDepthBlock(r) for r in (0.1, 0.5, 0.9)]
+    keep = torch.tensor([[1.0 - s.drop_rate] for s in sds])
+    torch.manual_seed(0)
+    d = cait.draw_stochastic_depth(sds, keep, 4096, torch.device("cpu"))
+    assert d.rows.shape == (3, 4096)
+    for i, s in enumerate(sds):
+        k = 1.0 - s.drop_rate
+        vals = d.rows[i].unique().tolist()
+        assert all(v == 0.0 or abs(v - 1.0 / k) < 1e-6 for v in vals)
+        assert abs(float((d.rows[i] > 0).float().mean()) - k) < 0.03
+    prev = cait._SD_DRAW
+    cait._SD_DRAW = d
+    try:
+        assert cait.sample_scale(4096, sds[1], True, torch.device("cpu")) is not None
+        assert torch.equal(cait.sample_scale(4096, sds[1], True, torch.device("cpu")), d.rows[1])
+        other = cait.StochasticDepthBlock(0.2)                      # not in the draw: its own
+        assert cait.sample_scale(4096, other, True, torch.device("cpu")).shape == (4096,)
+        assert cait.sample_scale(4096, sds[0], False, torch.device("cpu")) is None   # evaluation
+    finally:
+        cait._SD_DRAW = prev
