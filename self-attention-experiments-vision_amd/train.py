@@ -126,14 +126,18 @@ class FusedAdamW:
         # the tile path takes (K, N, column offsets multiples of 4)
         self.cast_groups, self.copies = [], []
         tiles_in = []
+        claimed = set()
         for ws in (cast_groups or []):
             K = ws[0].shape[0]
             ent = [slot.get(w.data_ptr()) for w in ws]
             if (any(e is None or e[1].numel() != w.numel() for e, w in zip(ent, ws))
+                    or any(e[0] in claimed for e in ent)          # a parameter is updated once
+                    or len({e[0] for e in ent}) != len(ent)
                     or any(w.dim() != 2 or w.shape[0] != K for w in ws)
                     or K % 4 or any(w.shape[1] % 4 for w in ws)
                     or any(e[2] % 16 or e[3] % 16 or e[4] % 16 or e[1].data_ptr() % 16 for e in ent)):
                 continue
+            claimed.update(e[0] for e in ent)
             N = sum(w.shape[1] for w in ws)
             w16 = torch.empty((K, N), dtype=torch.bfloat16, device=dev)
             wt16 = torch.empty((N, K), dtype=torch.bfloat16, device=dev)

@@ -213,6 +213,13 @@ def test_fused_adamw_cast_copies(dev):
     finally:
         opt_b.close()
     assert ops._wkey([b[2]]) not in ops._PERSIST
+    # a parameter named by two groups is updated once: the second group is left to the forward
+    c, fc = make()
+    opt_c = train.FusedAdamW(c, fc, cast_groups=[[c[2]], [c[2]], [c[0], c[0]]], **kw)
+    try:
+        assert [len(g) for g in opt_c.cast_groups] == [1]
+    finally:
+        opt_c.close()
 
 
 @pytest.mark.parametrize("model,graph", [("deit_ti_patch16", False), ("deit_ti_patch16", True), ("cait", True)])
