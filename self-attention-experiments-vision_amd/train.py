@@ -515,6 +515,15 @@ class TrainStep:
         # collectives while the capture runs: a "global" capture would refuse those queries
         # (hipErrorStreamCaptureUnsupported, fatal in the watchdog), a thread-local one allows them
         mode = "thread_local" if self.pg else "global"
+        if self.pg and self.collective in ("overlap", "between") and images.is_cuda:
+            # ... and querying a warm-up collective's event once the stream it was recorded on (the
+            # process group's internal stream) has begun capturing fails with hipErrorCapturedEvent,
+            # which terminates the process from the watchdog thread (seen intermittently at world 1).
+            # Retire the warm-up's collectives first: let the device drain and the watchdog (it
+            # polls every ~100 ms) drop every completed work before the capture starts.
+            import time
+            torch.cuda.synchronize()
+            time.sleep(1.0)
         try:
             if not self.two_graphs:     # the whole step (with the overlapped collectives) in one graph
                 g = torch.cuda.CUDAGraph()
