@@ -221,14 +221,18 @@ def relative_logits_indexed(qhat, rel_pos_emb_h, rel_pos_emb_w, Hs: int, Ws: int
 
 # ----------------------------------------------------------------- attention core (A3-A9)
 def attention_core_fwd(q, k, v, mode: str = "f64", scale: Optional[float] = None,
-                       th1=None, th2=None, bias=None, return_aux=False):
+                       th1=None, th2=None, bias=None, return_aux=False, round_scores: bool = True):
     """Core of ``AttentionBlock.__call__`` after the projections (attention.py:39-58).
 
     q [B,Nq,H,D], k/v [B,Nk,H,D] token-major.  ``scale`` defaults to the reference's
     division by sqrt(head_ch) (attention.py:39), applied to q **in dtype**.  Optional
     ``bias`` [B,H,Nq,Nk] is added to the logits (BoTNet relative logits, botnet.py:191).
     Optional talking-heads transforms th1/th2 [H,H] (attention.py:44-52).
-    Returns o [B,Nq,H,D] (and an aux dict with the logits / probabilities / LSE)."""
+    Returns o [B,Nq,H,D] (and an aux dict with the logits / probabilities / LSE).
+
+    ``round_scores=False`` (bf16 mode only) keeps the QK^T einsum's output in fp32 instead of
+    rounding it to bf16 as the reference's bf16 einsum does (attention.py:41-42): the arithmetic
+    of the HIP kernels, which exponentiate the fp32 MFMA accumulator."""
     D = q.shape[-1]
     qc, kc, vc = cast(q, mode), cast(k, mode), cast(v, mode)
     hi = "f64" if mode == "f64" else "f32"          # promoted type of fp32-param mixes
@@ -236,7 +240,8 @@ def attention_core_fwd(q, k, v, mode: str = "f64", scale: Optional[float] = None
         qh = cast(qc / np.sqrt(D).astype(_acc(mode)), mode)
     else:
         qh = cast(qc * _acc(mode)(scale), mode)
-    s = cast(np.einsum("bqhd,bkhd->bhqk", qh.astype(_acc(mode)), kc.astype(_acc(mode))), mode)
+    s = np.einsum("bqhd,bkhd->bhqk", qh.astype(_acc(mode)), kc.astype(_acc(mode)))
+    s = cast(s, mode) if round_scores else s
     pmode = mode
     s1 = s
     if bias is not None:
@@ -247,7 +252,8 @@ def attention_core_fwd(q, k, v, mode: str = "f64", scale: Optional[float] = None
     if th1 is not None:
         s1 = talking_heads_mix(th1, s1)      # fp32 param promotes (talking_heads.py:13)
         pmode = hi
-    p = softmax(s1, pmode)
+    # unrounded scores: the kernels' fp32 softmax (P rounded to bf16 only as the AV operand)
+    p = softmax(s1, pmode if round_scores or pmode != "bf16" else "f32")
     p2 = p
     if th2 is not None:
         p2 = talking_heads_mix(th2, p)

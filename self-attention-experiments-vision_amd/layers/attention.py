@@ -11,9 +11,10 @@ Same dataclass fields, same call signatures (``(inputs_q, inputs_kv, is_training
 cast to ``dtype`` for compute like Flax's DenseGeneral.  Parameters are created at
 construction when ``in_ch`` is given, otherwise at the first call (Flax ``init`` semantics).
 
-Compute path: projections go through ``ops.dense`` (forward and input gradient on the library
-GEMM, weight / bias gradients straight into fp32 by the split-token MFMA kernel
-``sae_gemm_dw``); the self-attention Q/K/V projection is ONE GEMM producing a packed
+Compute path: projections go through ``ops.dense`` (bf16 forward and input gradient on the
+hand-written ``sae_gemm_nt`` where ``ops.use_gemm_nt`` routes them -- every DeiT-S / CaiT shape --
+the wide ViT-B@384 shapes and the fp32 path on the library GEMM; weight / bias gradients straight
+into fp32 by the split-token MFMA kernel ``sae_gemm_dw``); the self-attention Q/K/V projection is ONE GEMM producing a packed
 [B, N, 3, H, D] buffer that the attention kernel reads in place by strides; the attention core
 is the fused HIP kernel (``ops.attention*``).  There is no eager/CPU fallback.
 """

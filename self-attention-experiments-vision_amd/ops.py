@@ -326,7 +326,11 @@ def _th_sinks(th1, th2):
     s1 = _sink(th1) if ok(th1) else None
     s2 = _sink(th2) if ok(th2) else None
     if s1 is not None and s2 is not None and s1.data_ptr() == s2.data_ptr():
-        s2 = None   # one parameter used as both transforms: autograd adds the two gradients
+        # one parameter used as both transforms: autograd adds the two gradients.  Sink neither:
+        # a sink counts as final the moment its kernel is enqueued (the overlapped all-reduce
+        # launches its bucket then), so sinking dT1 while autograd still adds dT2 into the same
+        # view would race the bucket's all-reduce; the post-accumulate hook marks it ready instead
+        s1 = s2 = None
     return s1, s2
 
 
@@ -664,14 +668,37 @@ def clear_weight_cache() -> None:
 _PERSIST = {}
 
 
-def register_persistent_casts(groups, w16s, wt16s) -> None:
+def register_persistent_casts(groups, w16s, wt16s, owner=None) -> None:
+    """Serve ``groups``' bf16 copies from ``w16s`` / ``wt16s`` (kept current by ``owner``, the
+    optimizer that writes them).  A later registration of the same weights takes over."""
     for ws, w16, wt16 in zip(groups, w16s, wt16s):
-        _PERSIST[_wkey(ws)] = [tuple(w._version for w in ws), w16, wt16, list(ws)]
+        _PERSIST[_wkey(ws)] = [tuple(w._version for w in ws), w16, wt16, list(ws), owner]
 
 
-def unregister_persistent_casts(groups) -> None:
+def unregister_persistent_casts(groups, owner=None) -> None:
+    """Stop serving ``groups``' copies -- only the entries ``owner`` registered (None: any)."""
     for ws in groups:
-        _PERSIST.pop(_wkey(ws), None)
+        e = _PERSIST.get(_wkey(ws))
+        if e is not None and (owner is None or e[4] is owner):
+            del _PERSIST[_wkey(ws)]
+
+
+def release_persistent_casts(params) -> None:
+    """Drop every registered group holding one of ``params`` (an optimizer that now updates them
+    without writing those copies takes them over: the copies would go stale)."""
+    ids = {p.data_ptr() for p in params}
+    for key in [k for k, e in _PERSIST.items() if any(w.data_ptr() in ids for w in e[3])]:
+        del _PERSIST[key]
+
+
+def persistent_casts_stale(groups) -> bool:
+    """True when a weight of a registered group was changed in place since its copies were
+    written (load_state_dict, copy_: the version counter moved)."""
+    for ws in groups:
+        e = _PERSIST.get(_wkey(ws))
+        if e is not None and e[0] != tuple(w._version for w in e[3]):
+            return True
+    return False
 
 
 def persistent_casts_fresh(groups) -> None:

@@ -70,7 +70,10 @@ def init_distributed():
                 with socket.socket() as sk:
                     sk.bind(("127.0.0.1", 0))
                     os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
-            dist.init_process_group(backend="nccl", rank=0, world_size=1)
+            dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        elif backend == "nccl":
+            # device_id: the communicator is created now (eagerly), not by the first collective
+            dist.init_process_group(backend=backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend=backend)
     elif torch.cuda.is_available():
@@ -114,6 +117,9 @@ class FusedAdamW:
         self.m = torch.zeros_like(flat_grad)
         self.v = torch.zeros_like(flat_grad)
         self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        # copies an earlier optimizer over these parameters registered would go stale under this
+        # one (it updates the weights through raw pointers): they stop being served
+        ops.release_persistent_casts(self.params)
         slot = {}
         for i, p in enumerate(self.params):
             g = p.grad
@@ -180,12 +186,15 @@ class FusedAdamW:
                                                  ctypes.byref(cnt)))
             self.n_tiles = int(cnt.value)
             self.tiles = torch.frombuffer(bytearray(ttab), dtype=torch.uint8).to(dev)
-            ops.register_persistent_casts(self.cast_groups, [c[0] for c in self.copies], [c[1] for c in self.copies])
+            # the owner token: unregistering (close, finalizer) removes only this optimizer's entries
+            self._owner = object()
+            ops.register_persistent_casts(self.cast_groups, [c[0] for c in self.copies], [c[1] for c in self.copies],
+                                          self._owner)
             ops.recast_persistent(self.cast_groups)   # the copies of the initial weights
             # the registry holds the weights (their addresses cannot be reused while registered);
             # it lets go of them with the optimizer
             import weakref
-            weakref.finalize(self, ops.unregister_persistent_casts, list(self.cast_groups))
+            weakref.finalize(self, ops.unregister_persistent_casts, list(self.cast_groups), self._owner)
 
     def step(self):
         from . import _lib as L
@@ -205,11 +214,20 @@ class FusedAdamW:
             from . import ops
             ops.recast_persistent(self.cast_groups)
 
+    def refresh_if_stale(self):
+        """Re-cast the copies if a weight was changed in place since they were written: a replayed
+        step graph does not contain the cast, so a load_state_dict / copy_ after the capture would
+        otherwise reach the forward only after the next update.  Host-side version check."""
+        if self.cast_groups:
+            from . import ops
+            if ops.persistent_casts_stale(self.cast_groups):
+                ops.recast_persistent(self.cast_groups)
+
     def close(self):
         """Stop serving the copies (the forward casts per call again)."""
         if self.cast_groups:
             from . import ops
-            ops.unregister_persistent_casts(self.cast_groups)
+            ops.unregister_persistent_casts(self.cast_groups, self._owner)
             self.cast_groups = []
 
     def state_tensors(self):
@@ -255,6 +273,15 @@ class TrainStep:
             self.collective = "overlap"
         if self.collective != "none" and not self.flat:
             raise ValueError("TrainStep: the collective path needs the flat gradient buffer")
+        # the gradient all-reduces run on a process group of their own, created with an eager
+        # communicator (device_id) and given no eager work before the capture: RCCL's watchdog
+        # thread then never holds an event recorded on that group's internal stream, which joins
+        # the step's capture (an event query on a capturing stream is hipErrorCapturedEvent,
+        # fatal in the watchdog).  The warm-up steps before the capture run without collectives.
+        self._cpg = None
+        self._comm_on = True
+        if self.collective in ("overlap", "between") and on_gpu:
+            self._cpg = dist.new_group(backend="nccl", device_id=params[0].device)
         self.two_graphs = self.collective in ("between", "host") or (self.collective == "none" and bool(two_graphs))
         if self.flat:
             # one flat fp32 gradient buffer, every .grad a 16-byte-aligned view into it (autograd
@@ -360,13 +387,15 @@ class TrainStep:
         lo, hi = self._buckets[b]
         t = self._flat[lo:hi]
         self._launched[b] = True
+        if not self._comm_on:   # the capture's warm-up steps: no collective
+            return
         if t.is_cuda:
             # the comm stream picks up everything enqueued so far on the compute stream (this
             # bucket's gradient kernels included) and runs the RCCL all-reduce beside the rest of
             # the backward; inside a graph capture this is a fork of the captured graph
             self._comm.wait_stream(torch.cuda.current_stream(t.device))
             with torch.cuda.stream(self._comm):
-                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._cpg)
         else:
             self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
 
@@ -450,7 +479,7 @@ class TrainStep:
     def _allreduce(self):
         """The all-reduce between two graphs ("between" / "host"); "overlap" runs it inside the
         backward and "none" has none."""
-        if self.collective in ("none", "overlap"):
+        if self.collective in ("none", "overlap") or not self._comm_on:
             return
         if self.collective == "host":
             # rehearsal of the multi-rank step on fewer GPUs (SAE_DIST_BACKEND=gloo): one explicit
@@ -461,7 +490,8 @@ class TrainStep:
             return
         # every bucket in flight at once on the process group's stream; the optimizer's graph
         # replay waits for them on the compute stream (no host synchronisation)
-        works = [dist.all_reduce(self._flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True) for lo, hi in self._buckets]
+        works = [dist.all_reduce(self._flat[lo:hi], op=dist.ReduceOp.SUM, group=self._cpg, async_op=True)
+                 for lo, hi in self._buckets]
         for w in works:
             w.wait()
 
@@ -483,9 +513,15 @@ class TrainStep:
                       for p in params if id(p) in had_state}
         s = torch.cuda.Stream(device=images.device)
         s.wait_stream(torch.cuda.current_stream(images.device))
-        with torch.cuda.stream(s):   # warm-up on a side stream (allocator / library / communicator state)
-            for _ in range(2):
-                self._eager(self._images, self._labels)
+        # warm-up on a side stream (allocator, library and optimizer state), collectives off: the
+        # gradient group stays free of eager work until its collectives are captured (above)
+        self._comm_on = False
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._eager(self._images, self._labels)
+        finally:
+            self._comm_on = True
         torch.cuda.current_stream(images.device).wait_stream(s)
         # the warm-up steps were only for the allocator and the optimizer's lazily created state:
         # put parameters and optimizer state back, so that the first call performs exactly ONE
@@ -511,19 +547,10 @@ class TrainStep:
                         v.zero_()
         if not self.flat:
             self.opt.zero_grad(set_to_none=True)
-        # with a process group, RCCL's watchdog thread keeps querying the events of the warm-up's
-        # collectives while the capture runs: a "global" capture would refuse those queries
-        # (hipErrorStreamCaptureUnsupported, fatal in the watchdog), a thread-local one allows them
+        # thread_local: RCCL's watchdog thread keeps querying the events of the default group's
+        # eager work (the parameter broadcast) while the capture runs; a "global" capture would
+        # refuse those queries (hipErrorStreamCaptureUnsupported, fatal in the watchdog)
         mode = "thread_local" if self.pg else "global"
-        if self.pg and self.collective in ("overlap", "between") and images.is_cuda:
-            # ... and querying a warm-up collective's event once the stream it was recorded on (the
-            # process group's internal stream) has begun capturing fails with hipErrorCapturedEvent,
-            # which terminates the process from the watchdog thread (seen intermittently at world 1).
-            # Retire the warm-up's collectives first: let the device drain and the watchdog (it
-            # polls every ~100 ms) drop every completed work before the capture starts.
-            import time
-            torch.cuda.synchronize()
-            time.sleep(1.0)
         try:
             if not self.two_graphs:     # the whole step (with the overlapped collectives) in one graph
                 g = torch.cuda.CUDAGraph()
@@ -555,6 +582,9 @@ class TrainStep:
         if self.collective == "overlap":
             from . import ops
             ops.set_sink_listener(None)
+        if self._cpg is not None and dist.is_initialized():
+            dist.destroy_process_group(self._cpg)
+            self._cpg = None
         if isinstance(self.opt, FusedAdamW):
             self.opt.close()
 
@@ -577,6 +607,8 @@ class TrainStep:
             self._images.copy_(images)
         if labels.data_ptr() != self._labels.data_ptr():
             self._labels.copy_(labels)
+        if isinstance(self.opt, FusedAdamW):
+            self.opt.refresh_if_stale()
         self._g.replay()
         if self._g_opt is not None:
             self._allreduce()

@@ -5,7 +5,8 @@ pmap(train_step) + lax.pmean(grads), train.py:94-96,230: flat gradient buffer, b
 all-reduce of the gradients of loss / world) must give every rank the same parameters as a
 single process stepping on the concatenated global batch (global-mean gradient, survey D9),
 starting from rank 0's initial state whatever the other ranks initialised.
-The GPU step runs the same code between its two HIP graphs.  The attention kernels themselves are replicas (GPU only); this checks the
+On the GPU the same bucket logic runs inside the captured step graph (the all-reduces forked onto a
+communication stream).  The attention kernels themselves are replicas (GPU only); this checks the
 collective / bucketing / optimizer path with a small CPU model.
 """
 import os
@@ -15,6 +16,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+from sae_vision_amd import ops as _ops
 
 
 class TinyNet(torch.nn.Module):
@@ -97,3 +100,109 @@ def test_smoothed_cross_entropy_matches_optax_formula():
     y = torch.nn.functional.one_hot(labels, 10).double() * 0.9 + 0.1 / 10      # optax.smooth_labels
     ref = -(y * torch.log_softmax(logits, -1)).sum(-1).mean()
     torch.testing.assert_close(train.smoothed_cross_entropy(logits, labels, 0.1).double(), ref)
+
+
+class _MixTH(torch.autograd.Function):
+    """A CPU stand-in for the talking-heads op's gradient handling (ops._TalkingHeads): y = x T1 +
+    x T2 with the transforms' gradients going through ops._th_sinks / _claim / _unsunk exactly as
+    the HIP op's backward does (the sink written in place, the listener told via ops._sinking)."""
+
+    @staticmethod
+    def forward(ctx, x, t1, t2):
+        from sae_vision_amd import ops
+        ctx.save_for_backward(x, t1, t2)
+        ctx.sinks = ops._th_sinks(t1, t2)
+        return x @ t1 + x @ t2
+
+    @staticmethod
+    @_ops._sinking
+    def backward(ctx, dy):
+        from sae_vision_amd import ops
+        x, t1, t2 = ctx.saved_tensors
+        g = x.t() @ dy
+        s1, s2 = ctx.sinks
+        s1, s2 = ops._claim(s1), ops._claim(s2)
+        if s1 is not None:
+            s1.copy_(g)
+        if s2 is not None:
+            s2.copy_(g)
+        return dy @ (t1 + t2).t(), ops._unsunk(g.clone(), s1), ops._unsunk(g.clone(), s2)
+
+
+class AliasTHNet(torch.nn.Module):
+    """One [H, H] parameter used as BOTH transforms (a shared talking-heads transform)."""
+
+    def __init__(self, seed: int = 0):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.l1 = torch.nn.Linear(12, 8)
+        self.t = torch.nn.Parameter(torch.randn(8, 8) * 0.3)
+        self.l2 = torch.nn.Linear(8, 5)
+
+    def forward(self, x, is_training: bool):
+        return self.l2(_MixTH.apply(self.l1(x.flatten(1)), self.t, self.t))
+
+
+def _alias_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from sae_vision_amd import train
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, y = _data()
+    per = x.shape[0] // world
+    step = train.TrainStep(AliasTHNet(seed=rank), global_batch=x.shape[0], bucket_cap_mb=0.0001)
+    assert step.collective == "overlap"
+    ti = [i for i, p in enumerate(step._params) if p is step.model.t][0]
+    lo, hi = step._offs[ti], step._offs[ti] + step.model.t.numel()
+    seen = []
+    orig = step._launch_bucket
+
+    def spy(bi):
+        blo, bhi = step._buckets[bi]
+        if blo <= lo and hi <= bhi:   # the bucket holding the shared transform: its gradient as launched
+            seen.append(step._flat[lo:hi].clone())
+        return orig(bi)
+    step._launch_bucket = spy
+    for _ in range(2):
+        step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+        assert seen and torch.isfinite(seen[-1]).all()
+    flat = torch.cat([p.detach().flatten() for p in step.model.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save({"params": torch.stack(gathered)}, out)
+    dist.destroy_process_group()
+
+
+def test_aliased_transform_bucket_waits_for_accumulation(tmp_path):
+    """a parameter fed to one op as both talking-heads transforms must not count as
+    final when dT1's sink is written -- autograd still adds dT2.  With the fix neither is sunk and
+    the post-accumulate hook releases the bucket; the 2-rank result equals the single process."""
+    from sae_vision_amd import ops, train
+    out = str(tmp_path / "alias.pt")
+    mp.spawn(_alias_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    assert torch.equal(got["params"][0], got["params"][1]), "ranks diverged"
+    x, y = _data()
+    ref = train.TrainStep(AliasTHNet(), global_batch=x.shape[0])
+    for _ in range(2):
+        ref(x, y)
+    flat = torch.cat([p.detach().flatten() for p in ref.model.parameters()])
+    torch.testing.assert_close(got["params"][0], flat, rtol=1e-5, atol=1e-6)
+    # the sink decision itself: one parameter as both transforms -> neither sunk
+    p = torch.nn.Parameter(torch.zeros(4, 4))
+    p.grad = torch.zeros(4, 4)
+    ops.set_grad_sinks([p], [p.grad])
+    ops.begin_backward_sinks()
+    try:
+        assert ops._th_sinks(p, p) == (None, None)
+        q = torch.nn.Parameter(torch.zeros(4, 4))
+        q.grad = torch.zeros(4, 4)
+        ops.set_grad_sinks([q], [q.grad])
+        s1, s2 = ops._th_sinks(p, q)
+        assert s1 is not None and s2 is not None
+    finally:
+        ops.end_backward_sinks()
+        ops.set_grad_sinks(None)

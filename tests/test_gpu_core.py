@@ -127,11 +127,19 @@ def test_deterministic(dev, N):
 
 
 @pytest.mark.parametrize("mode", ["f32", "bf16"])
-@pytest.mark.parametrize("gain", [0.05, 0.6, 4.0])
+@pytest.mark.parametrize("gain", [0.05, 0.6, 4.0, 6.0, 8.0])
 def test_softmax_spike(dev, mode, gain):
     """Forces the online-softmax max to jump at a late key tile (rule 26): gain 4 jumps far past
     the lazy-rescale threshold (rescale branch; ~46 log2 units, inside the bf16 forward's
-    fixed-max range), gain 0.6 jumps by a few log2 units (P > 1 path), gain 0.05 barely moves it."""
+    fixed-max range), gains 6 / 8 up to ~70 / ~92 log2 units (past it: the fixed-max fallback
+    sweep), gain 0.6 jumps by a few log2 units (P > 1 path), gain 0.05 barely moves it.
+
+    bf16 rounding of the scores: the reference's bf16 einsum rounds S to
+    bf16 before the softmax (attention.py:41-42); the kernels exponentiate the fp32 MFMA
+    accumulator.  At large logits that rounding alone moves the reference's output by more than
+    the 2e-2 bar (gain 8: the bf16-emulated oracle is 0.024 from float64, 0.025 from the same
+    program with fp32 scores), so the bf16 forward is pinned to the oracle with unrounded scores
+    at 2e-2 AND must be at least as close to float64 as the reference's own bf16 program."""
     import torch
     import sae_vision_amd.ops as ops
 
@@ -150,7 +158,12 @@ def test_softmax_spike(dev, mode, gain):
     o = ops.attention(tq, tk, tv)
     do = randn(np.random.default_rng(2), (B, N, H, D), mode)
     o.backward(torch.tensor(do, device=dev, dtype=td))
-    assert rel_err(o, R.attention_core_fwd(q, k, v, "f64" if mode == "f32" else "bf16")) <= TOL[mode]
+    o64 = R.attention_core_fwd(q, k, v, "f64")
+    if mode == "f32":
+        assert rel_err(o, o64) <= TOL[mode]
+    else:
+        assert rel_err(o, R.attention_core_fwd(q, k, v, "bf16", round_scores=False)) <= TOL[mode]
+        assert rel_err(o, o64) <= max(TOL[mode], rel_err(R.attention_core_fwd(q, k, v, "bf16"), o64))
     g = R.attention_core_bwd(q, k, v, do)
     for n, t in (("dq", tq), ("dk", tk), ("dv", tv)):
         assert rel_err(t.grad, g[n]) <= TOL[mode], n

@@ -249,3 +249,32 @@ def test_train_step_persistent_casts_bitwise(dev, model, graph):
             assert torch.equal(pa, pb), n
     finally:
         s_b.opt.close()
+
+
+def test_graph_step_sees_weights_loaded_after_capture(dev):
+    """a replayed step graph holds no weight cast (the optimizer writes the bf16
+    copies), so weights loaded in place after the capture (load_state_dict) must re-cast the
+    copies before the next replay: the step after the load equals, bit for bit, a step that casts
+    every forward (persistent_casts=False) from the same loaded state."""
+    from sae_vision_amd import train, vit
+    torch.manual_seed(0)
+    m_a = vit.create_model("deit_ti_patch16", 1000, torch.bfloat16, device=dev)
+    m_b = copy.deepcopy(m_a)
+    fresh = copy.deepcopy(m_a).state_dict()          # the state loaded mid-run
+    s_a = train.TrainStep(m_a, global_batch=8, device=dev, graph=True, persistent_casts=False)
+    s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=True)
+    g = torch.Generator(device=dev).manual_seed(7)
+    data = [(torch.randn(8, 224, 224, 3, device=dev, generator=g),
+             torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
+    try:
+        for m, s in ((m_a, s_a), (m_b, s_b)):
+            s(*data[0])                                  # capture + first replay
+            s(*data[1])
+            m.load_state_dict(fresh)                     # in place: same storage, versions move
+        la, lb = float(s_a(*data[2])), float(s_b(*data[2]))
+        assert la == lb, (la, lb)
+        for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
+            assert torch.equal(pa, pb), n
+    finally:
+        s_b.close()
+        s_a.close()

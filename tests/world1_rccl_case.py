@@ -34,7 +34,7 @@ def main(model):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)   # as train.init_distributed
     s_b = None
     try:
         s_b = train.TrainStep(m_b, global_batch=8, device=dev, graph=True, bucket_cap_mb=4.0)
