@@ -1,0 +1,284 @@
+// gemm8.h -- the projection / FF GEMMs on 256-row tiles of one 8-wave workgroup per CU.
+//
+//   c[m][n] = epi( sum_k a[m][k] * bt[n][k] (+ bias[n]) )          (NtArgs, gemm_nt.h epilogues)
+//
+// Why a second GEMM structure: sae_gemm_nt's 128 x 128 tiles read 64 FLOP per
+// L2 byte, so at two workgroups per CU the operand stream from L2 takes as long as the MFMAs
+// (profiles/r02_pmc_gemm_nt.txt: MFMA busy 0.23).  Here a workgroup owns a 256 x BN tile (BN = 128,
+// 192 or 256: 85 / 110 / 128 FLOP per L2 byte) and its 8 waves (2 per SIMD) share one LDS ring:
+//   * operands staged by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction, no VGPR
+//     round trip), NS stage buffers of BK-deep A [256][BK] and B [BN][BK] images, NS - 1 stages in
+//     flight; each wave waits with a counted vmcnt for its own pieces of the stage it is about to
+//     read, one s_barrier per stage publishes them and frees the buffer the next issue overwrites;
+//   * 16-byte chunks of the images XOR-swizzled per row through the DMA SOURCE address (the DMA
+//     writes lane-linearly), so the v_mfma_f32_16x16x32_bf16 fragment reads (ds_read_b128, 16 rows
+//     x 4 chunks per wave-instruction) are bank-conflict free;
+//   * waves as 2 (M) x 4 (N): wave tile 128 x BN / 4, accumulators D = C^T (the output feature on
+//     the accumulator row, the token on the lane), so the epilogue writes each token's features
+//     as bf16x4 into a per-wave LDS image and stores whole row segments (16 B per lane);
+//   * waves 4-7 (the second half to be dispatched, which loses VALU arbitration to its SIMD
+//     partner) run at s_setprio 1 for the main loop (MI355X_MICROARCH.md, two waves per SIMD,
+//     item 4).
+#pragma once
+#include "gemm_nt.h"
+
+namespace sae {
+
+typedef __attribute__((ext_vector_type(4))) unsigned g8_u32x4;
+
+// descriptor words over rows [0, nrows) of a [rows][ld] bf16 operand (range check = zero fill)
+__device__ __forceinline__ g8_u32x4 g8_rsrc(const __bf16* base, int nrows, long long ld) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  g8_u32x4 w;
+  w[0] = __builtin_amdgcn_readfirstlane((unsigned)p);
+  w[1] = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32)) & 0xffffu;
+  w[2] = __builtin_amdgcn_readfirstlane((unsigned)((long long)nrows * ld * 2));
+  w[3] = 0x00020000u;
+  return w;
+}
+
+// one 1-KiB LDS-DMA piece: lane L's 16 bytes (global byte offset voff in the descriptor's range)
+// land at LDS byte address lds + 16 L.  M0 is saved / restored inside the statement.
+__device__ __forceinline__ void g8_dma1(g8_u32x4 rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ void g8_dma2(g8_u32x4 rs, unsigned voff0, unsigned voff1, unsigned lds0, unsigned lds1) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff0), "v"(voff1), "s"(rs), "s"(lds0), "s"(lds1)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void g8_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// chunk swizzle of a BK-deep bf16 image row (BK = 32: 64-byte rows, BK = 64: 128-byte rows),
+// chosen for the 16x16x32 fragment read: lane l reads row base + (l & 15), chunk 4 kk + (l >> 4);
+// within each 16-lane group of a ds_read_b128 the 16 chunks then hit distinct 16-byte bank slots
+template <int BK> __device__ __forceinline__ int g8_swz(int r) {
+  if constexpr (BK == 32) return (0x1320 >> (4 * ((r >> 2) & 3))) & 3;   // [0, 2, 3, 1][(r >> 2) & 3]
+  else return (r >> 1) & 7;
+}
+
+template <int BN> struct G8Cfg {
+  static constexpr int BM = 256;
+  static constexpr int WM = 128, WN = BN / 4;     // wave tile (2 x 4 waves)
+  static constexpr int MT = WM / 16, NT = WN / 16; // 16 x 16 accumulator tiles per wave
+};
+
+// LDS: the stage ring, then one 32-row epilogue scratch per wave (rows padded by 16 bytes)
+template <int BN, int BK, int NS> constexpr int g8_ring_bytes() { return NS * (256 + BN) * BK * 2; }
+template <int BN> constexpr int g8_scratch_bytes() { return 32 * (BN / 4 * 2 + 16); }
+template <int BN, int BK, int NS> constexpr int g8_lds_bytes() {
+  return g8_ring_bytes<BN, BK, NS>() + 8 * g8_scratch_bytes<BN>();
+}
+
+// Persistent: workgroup b walks tiles xcd_remap(b) + i G (G = gridDim.x <= #tiles; consecutive
+// logical tiles -- the N tiles of one 256-row block -- run on one XCD at the same time, so the A
+// rows come from HBM once per XCD).  The stage stream runs on across tiles: the next tile's first
+// NS - 1 stages are in flight while a tile's epilogue drains its accumulators (through the
+// per-wave scratch, 32 rows at a time: 16-byte row-segment stores), so neither the prologue's load
+// latency nor the epilogue's stores stall the ring.
+template <int EPI, int BN, int BK, int NS>
+__global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using C = G8Cfg<BN>;
+  constexpr int RB = BK * 2;                  // image row bytes
+  constexpr int CPR = BK / 8;                 // 16-byte chunks per row
+  constexpr int RPP = 64 / CPR;               // rows per 1-KiB piece
+  constexpr int IMGA = 256 * RB, STAGE = (256 + BN) * RB;
+  constexpr int PA = 256 / RPP / 8;           // A pieces per wave per stage
+  constexpr int PBT = BN / RPP;               // B pieces per stage (all waves)
+  static_assert(PA * RPP * 8 == 256, "A pieces");
+  constexpr int PB0 = (PBT + 7) / 8;          // B pieces of waves 0 .. PBT % 8 - 1
+  constexpr int PB1 = PBT / 8;                // B pieces of the other waves
+  constexpr int PBX = PBT % 8;                // waves with PB0 pieces (0: every wave has PB1)
+
+  const int tn = (a.N + BN - 1) / BN;
+  const int ntiles = ((a.M + 255) / 256) * tn;
+  const int G = gridDim.x;
+  const int b0 = xcd_remap(blockIdx.x, G);
+  const int myt = (ntiles - b0 + G - 1) / G;  // tiles of this workgroup: b0, b0 + G, ...
+  const int nst = a.K / BK;
+  const int total = myt * nst;                // stages of this workgroup's stream
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const unsigned lbase = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  // this wave's pieces: A pieces w + 8 i (rows RPP (w + 8 i) ...), B pieces w + 8 i
+  const int prow = lane / CPR, pc = lane % CPR;
+  unsigned goa[PA], gob[PB0 > 0 ? PB0 : 1];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int row = RPP * (w + 8 * i) + prow;
+    goa[i] = (unsigned)(((long long)row * a.lda + 8 * (pc ^ g8_swz<BK>(row))) * 2);
+  }
+#pragma unroll
+  for (int i = 0; i < (PB0 > 0 ? PB0 : 1); ++i) {
+    const int row = RPP * (w + 8 * i) + prow;
+    gob[i] = (unsigned)(((long long)row * a.ldb + 8 * (pc ^ g8_swz<BK>(row))) * 2);
+  }
+  const bool bx = PBX == 0 || w < PBX;   // this wave issues PB0 B pieces (else PB1)
+
+  // issue cursor: stage ist of local tile iti, with that tile's descriptors
+  int iti = 0, ist = 0, ibuf = 0;
+  g8_u32x4 ra, rb;
+  auto set_issue_tile = [&](int it) {
+    const int t = b0 + it * G;
+    const int m0 = (t / tn) * 256, n0 = (t % tn) * BN;
+    ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(256, a.M - m0), a.lda);
+    rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
+  };
+  auto issue_next = [&]() {
+    const unsigned ko = (unsigned)ist * RB;
+    const unsigned lb = lbase + (unsigned)(ibuf * STAGE);
+#pragma unroll
+    for (int i = 0; i < PA; i += 2) {
+      if (i + 1 < PA)
+        g8_dma2(ra, goa[i] + ko, goa[i + 1] + ko, lb + 1024u * (w + 8 * i), lb + 1024u * (w + 8 * (i + 1)));
+      else
+        g8_dma1(ra, goa[i] + ko, lb + 1024u * (w + 8 * i));
+    }
+#pragma unroll
+    for (int i = 0; i < PB0; ++i) {
+      if (i < PB1 || bx) g8_dma1(rb, gob[i] + ko, lb + IMGA + 1024u * (w + 8 * i));
+    }
+    ibuf = ibuf + 1 == NS ? 0 : ibuf + 1;
+    if (++ist == nst) {
+      ist = 0;
+      if (++iti < myt) set_issue_tile(iti);
+    }
+  };
+
+  f32x4 acc[C::MT][C::NT];
+#pragma unroll
+  for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row base + (lane & 15), chunk 4 kk + (lane >> 4)
+  const int fr = lane & 15, fg = lane >> 4;
+  const int sw = g8_swz<BK>(fr);   // rows are 16-aligned + fr: the swizzle depends on fr only
+  const char* pa0 = smem + (128 * wr + fr) * RB;
+  const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB;
+  constexpr int SRB = C::WN * 2 + 16;             // scratch row bytes (wave tile row + pad)
+  constexpr int SCH = C::WN / 8;                  // 16-byte chunks per tile row
+  char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN>();
+
+  if (myt > 0) set_issue_tile(0);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < total) issue_next();
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  int cur = 0, cst = 0, cti = 0;   // compute cursor: buffer, stage, local tile
+  for (int g = 0; g < total; ++g) {
+    // stage g landed (this wave's pieces; the barrier: everyone's), buffer of g - 1 free
+    const int ahead = min(NS - 2, total - 1 - g);   // younger stages still in flight
+    if (ahead >= 2) {
+      if (bx) g8_wait_barrier<2 * (PA + PB0)>(); else g8_wait_barrier<2 * (PA + PB1)>();
+    } else if (ahead == 1) {
+      if (bx) g8_wait_barrier<PA + PB0>(); else g8_wait_barrier<PA + PB1>();
+    } else {
+      g8_wait_barrier<0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + NS - 1 < total) issue_next();
+    const char* ia = pa0 + cur * STAGE;
+    const char* ib = pb0 + cur * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int co = 16 * ((4 * kk + fg) ^ sw);
+      bf16x8 bf[C::NT], af[C::MT];
+#pragma unroll
+      for (int j = 0; j < C::NT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(ib + 16 * j * RB + co);
+#pragma unroll
+      for (int i = 0; i < C::MT; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * i * RB + co);
+#pragma unroll
+      for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    cur = cur + 1 == NS ? 0 : cur + 1;
+    if (++cst < nst) continue;
+    cst = 0;
+
+    // ---- epilogue of local tile cti.  acc[i][j] = D[n][m]: n = WN wc + 16 j + 4 fg + e,
+    // m = 128 wr + 16 i + fr (tile-relative); through the wave's scratch 32 rows at a time
+    const int t = b0 + cti * G;
+    ++cti;
+    const int m0 = (t / tn) * 256 + 128 * wr, nw = (t % tn) * BN + C::WN * wc;
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    f32x4 bv[C::NT];
+#pragma unroll
+    for (int j = 0; j < C::NT; ++j) {
+      const int n = nw + 16 * j + 4 * fg;
+      bv[j] = (EPI != kEpiDGelu && a.bias && n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n)
+                                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int ip = 0; ip < C::MT / 2; ++ip) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int i = 2 * ip + h2;
+#pragma unroll
+        for (int j = 0; j < C::NT; ++j) {
+          const bf16x4 v = {(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
+                            (__bf16)(acc[i][j][2] + bv[j][2]), (__bf16)(acc[i][j][3] + bv[j][3])};
+          *reinterpret_cast<bf16x4*>(scratch + (16 * h2 + fr) * SRB + 2 * (16 * j + 4 * fg)) = v;
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int it = 0; it < 32 * SCH / 64; ++it) {
+        const int id = it * 64 + lane;
+        const int rr = id / SCH, c = id % SCH;
+        const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * SRB + 16 * c);
+        const int m = m0 + 32 * ip + rr, n = nw + 8 * c;
+        if (m < a.M && n < a.N) {
+          if constexpr (EPI == kEpiNone) {
+            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
+          } else if constexpr (EPI == kEpiGelu) {
+            *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
+            const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
+            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+          } else {
+            const uint4 hv = *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n);
+            const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
+                             dgelu_bf2(raw.w, hv.w)};
+            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (w >= 4) __builtin_amdgcn_s_setprio(0);
+}
+
+}  // namespace sae

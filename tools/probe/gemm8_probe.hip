@@ -1,0 +1,56 @@
+// Probe build of gemm8.h variants (dev only: tools/probe/gemm8_probe.py loads it by ctypes).
+#include <cstring>
+#include <algorithm>
+#include "../../self-attention-experiments-vision_amd/csrc/gemm8.h"
+
+using namespace sae;
+static int g_persist = 0;   // > 0: persistent grid of at most that many workgroups
+
+template <int EPI, int BN, int BK, int NS>
+static int launch(const NtArgs& g, hipStream_t st) {
+  constexpr int lds = g8_lds_bytes<BN, BK, NS>();
+  const void* fn = (const void*)gemm8_nt_kernel<EPI, BN, BK, NS>;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return 2;
+  const long long tiles = (long long)((g.M + 255) / 256) * ((g.N + BN - 1) / BN);
+  const long long grid = g_persist ? std::min<long long>(tiles, g_persist) : tiles;
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+template <int BN, int BK, int NS>
+static int launch_epi(const NtArgs& g, int epi, hipStream_t st) {
+  if (epi == 0) return launch<kEpiNone, BN, BK, NS>(g, st);
+  if (epi == 1) return launch<kEpiGelu, BN, BK, NS>(g, st);
+  return launch<kEpiDGelu, BN, BK, NS>(g, st);
+}
+
+extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void* a, long long lda, const void* bt,
+                      long long ldb, const float* bias, void* c, long long ldc, int epi, const void* aux,
+                      long long ldaux, void* c2) {
+  NtArgs g;
+  memset(&g, 0, sizeof g);
+  g.a = (const __bf16*)a;
+  g.bt = (const __bf16*)bt;
+  g.bias = bias;
+  g.aux = (const __bf16*)aux;
+  g.c = (__bf16*)c;
+  g.c2 = (__bf16*)c2;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.ldaux = ldaux;
+  hipStream_t st = (hipStream_t)stream;
+  g_persist = variant >= 10 ? 256 : 0;
+  switch (variant % 10) {
+    case 0: return launch_epi<256, 32, 3>(g, epi, st);
+    case 1: return launch_epi<192, 32, 3>(g, epi, st);
+    case 2: return launch_epi<192, 32, 4>(g, epi, st);
+    case 3: return launch_epi<192, 64, 2>(g, epi, st);
+    case 4: return launch_epi<128, 32, 4>(g, epi, st);
+    case 5: return launch_epi<128, 64, 2>(g, epi, st);
+  }
+  return 1;
+}
