@@ -22,6 +22,7 @@
 #include "cls.h"
 #include "gemm_dw.h"
 #include "gemm_nt.h"
+#include "gemm8.h"
 #include "loss.h"
 #include "tokens.h"
 #include "patch.h"
@@ -534,6 +535,41 @@ static int nt_launch(const NtArgs& g, long long grid, hipStream_t st) {
   if (int rc = lds_attr((const void*)gemm_nt_kernel<EPI, AL>, lds)) return rc;
   hipLaunchKernelGGL((gemm_nt_kernel<EPI, AL>), dim3((unsigned)grid), dim3(256), lds, st, g);
   return 0;
+}
+
+// compute units of the current device (persistent grids), cached per device
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// one persistent gemm8 launch (256 x BN tiles, one 8-wave workgroup per CU)
+template <int EPI, int BN, int BK, int NS>
+static int g8_launch(const NtArgs& g, hipStream_t st) {
+  constexpr int lds = g8_lds_bytes<BN, BK, NS>();
+  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS>, lds)) return rc;
+  const long long tiles = (long long)((g.M + 255) / 256) * ((g.N + BN - 1) / BN);
+  const long long grid = std::min<long long>(tiles, device_cus());
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  return 0;
+}
+
+// gemm8 (gemm8.h) or the 128-row sae_gemm_nt: tools/probe/gemm8_probe.py, profiles/r04c_g8probe.txt --
+// gemm8 wins on the 384-feature outputs at every depth (DeiT-S / CaiT output projection, QKV and
+// FF Dense_0 input gradients, Dense_1 forward: 412-692 -> 497-849 TF/s) and on the wide K = 768
+// ViT-B forwards (QKV 2304 features 750 -> 850-900, FF Dense_0 + GELU 673-700 -> 715-729: level with
+// the library's 830-960); the 128-row kernel stays on the DeiT-S wide K = 384 outputs (a tie) and
+// the GELU' epilogue (gemm8 has none)
+static bool g8_route(int M, int N, int K, int epilogue) {
+  if (epilogue == SAE_EPI_DGELU || N % 192 || K % 64 || K < 384 || M < 4096) return false;
+  return N == 384 || (K >= 768 && N >= 1152 && N <= 3072);
 }
 
 extern "C" {
@@ -1079,6 +1115,16 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   g.ldc = ldc;
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
+  if (g8_route(M, N, K, epilogue)
+#ifdef SAE_DEV_KNOBS
+      && !dev_knob("SAE_NT_NO_G8")
+#endif
+  ) {
+    const int rc = epilogue == SAE_EPI_NONE ? g8_launch<kEpiNone, 192, 64, 2>(g, st)
+                                            : g8_launch<kEpiGelu, 192, 64, 2>(g, st);
+    if (rc) return rc;
+    return check_launch("gemm8_nt");
+  }
   // tile height: 256 tokens for the GELU / GELU' epilogue GEMMs at K >= 768 (the ViT-B FF block:
   // the epilogue's VALU work per output is amortised over twice the MFMA work per tile;
   // tools/nt_probe.py at M 36928 K 768 N 3072: GELU 512 -> 634, GELU' 548 -> 609 TF/s) when that

@@ -942,8 +942,12 @@ GEMM_NT_NARROW_MAX_K = 1536
 
 
 def use_gemm_nt(K: int, N: int) -> bool:
-    """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt."""
-    return GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
+    """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt.
+    Round 4: the wide K = 768 outputs (ViT-B QKV forward, N 2304; FF Dense_0, N 3072) go to it as
+    well -- the C-ABI runs them on the 256-row persistent gemm8 kernel, level with the library
+    (profiles/r04c_g8probe.txt); the 768-feature outputs at K >= 768 stay on the library."""
+    return (GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
+            or (K == 768 and N % 192 == 0 and 1152 <= N <= 3072))
 
 
 def _nt_ok(a2: torch.Tensor, N: int) -> bool:

@@ -219,3 +219,48 @@ def test_gemm_nt_odd_stages_repeatable(dev, K):
     assert _rel(first, ref) <= 1e-2
     for _ in range(20):
         assert torch.equal(ops.gemm_nt(a, bt, b), first)
+
+
+# gemm8.h (the persistent 256-row kernel sae_gemm_nt routes the 384-feature outputs and the wide
+# K = 768 forwards to): one tile per workgroup (25216 x 384: 198 tiles), several per workgroup
+# (70000 x 384: 548 tiles; 18464 x 2304: 1,152 tiles), ragged last row block (5000, 70000, 18464)
+G8_SHAPES = [(25216, 384, 384), (25216, 1152, 384), (25216, 1536, 384), (5000, 384, 384), (70000, 384, 384),
+             (18464, 768, 2304)]
+
+
+@pytest.mark.parametrize("M,K,N", G8_SHAPES)
+def test_gemm8_plain_repeatable(dev, M, K, N):
+    """gemm8: against the float64 product (bias in the first K-tile's MFMA C operand) and bit-equal
+    over reruns (a stage read before its LDS-DMA landed shows up as run-to-run differences)."""
+    import sae_vision_amd.ops as ops
+    a, bt, b = _inputs(dev, M, K, N, 3 * M + K)
+    ref = a.double() @ bt.double().t() + b.double()
+    first = ops.gemm_nt(a, bt, b)
+    assert _rel(first, ref) <= 1e-2
+    for _ in range(5):
+        assert torch.equal(ops.gemm_nt(a, bt, b), first)
+    assert _rel(ops.gemm_nt(a, bt), a.double() @ bt.double().t()) <= 1e-2   # no bias
+
+
+@pytest.mark.parametrize("M,K,N", [(18464, 768, 3072), (3000, 768, 1152)])
+def test_gemm8_gelu(dev, M, K, N):
+    import sae_vision_amd.ops as ops
+    a, bt, b = _inputs(dev, M, K, N, 17)
+    y, h = ops.gemm_nt(a, bt, b, ops.EPI_GELU)
+    assert _rel(h, a.double() @ bt.double().t() + b.double()) <= 1e-2
+    ref_y = F.gelu(h.float(), approximate="tanh")
+    assert float((y.float() - ref_y).abs().max()) <= 2 ** -7 * float(ref_y.abs().max())
+
+
+def test_gemm8_strided(dev):
+    """gemm8 with a row-strided a and c written into a wider buffer (columns outside untouched)."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(6)
+    M, K, N = 9000, 384, 384
+    aw = torch.randn(M, K + 64, device=dev, generator=g).to(torch.bfloat16)
+    a = aw[:, 64:]
+    bt = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).to(torch.bfloat16)
+    cw = torch.full((M, N + 64), 3.0, device=dev, dtype=torch.bfloat16)
+    ops.gemm_nt(a, bt, out=cw[:, 32:32 + N])
+    assert _rel(cw[:, 32:32 + N], a.double() @ bt.double().t()) <= 1e-2
+    assert torch.all(cw[:, :32] == 3.0) and torch.all(cw[:, 32 + N:] == 3.0)

@@ -6,14 +6,14 @@
 using namespace sae;
 static int g_persist = 0;   // > 0: persistent grid of at most that many workgroups
 
-template <int EPI, int BN, int BK, int NS>
+template <int EPI, int BN, int BK, int NS, int MODE = 0>
 static int launch(const NtArgs& g, hipStream_t st) {
   constexpr int lds = g8_lds_bytes<BN, BK, NS>();
-  const void* fn = (const void*)gemm8_nt_kernel<EPI, BN, BK, NS>;
+  const void* fn = (const void*)gemm8_nt_kernel<EPI, BN, BK, NS, MODE>;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return 2;
   const long long tiles = (long long)((g.M + 255) / 256) * ((g.N + BN - 1) / BN);
   const long long grid = g_persist ? std::min<long long>(tiles, g_persist) : tiles;
-  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, MODE>), dim3((unsigned)grid), dim3(512), lds, st, g);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -44,6 +44,14 @@ extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
   g_persist = variant >= 10 ? 256 : 0;
+  if (variant >= 20) {   // staging / store experiments on the persistent 256 x 192 bk64 ns2 tile
+    g_persist = 256;
+    if (variant == 21) return epi == 0 ? launch<kEpiNone, 192, 64, 2, 1>(g, st) : 1;
+    if (variant == 22) return epi == 0 ? launch<kEpiNone, 192, 64, 2, 2>(g, st) : 1;
+    if (variant == 23) return epi == 0 ? launch<kEpiNone, 256, 32, 3, 1>(g, st) : 1;
+    if (variant == 24) return epi == 0 ? launch<kEpiNone, 256, 32, 3, 2>(g, st) : 1;
+    return 1;
+  }
   switch (variant % 10) {
     case 0: return launch_epi<256, 32, 3>(g, epi, st);
     case 1: return launch_epi<192, 32, 3>(g, epi, st);
