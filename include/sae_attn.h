@@ -203,6 +203,23 @@ int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t j
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
                 const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
                 int32_t epilogue, const void* aux, int64_t ldaux, void* c2);
+/* The same projections at compute dtype float32 (the reference's fp32 trunks, cait.py:147-154,
+   and every fp32 run), on the exact-f32 MFMA:
+     c[m][n] = (accumulate ? c[m][n] : 0) + sum_k A(m,k) B(k,n) (+ bias[n])
+     A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn]
+   One stride of each operand must be 1 (sak == 1: k-contiguous, else sam == 1), the other a
+   multiple of 4 covering the contiguous extent, that extent (K, M or N) a multiple of 4; a and b
+   16-byte aligned; c fp32 [M][ldc]; bias fp32 [N] or NULL.  colsum != NULL also writes
+   colsum[n] (+)= sum_k B(k,n) (a weight gradient's db beside its dW, one pass).  Deep, narrow
+   shapes split K over sae_gemm_f32_workspace_bytes(M, N, K) bytes of workspace (0: none
+   needed) with a fixed-order reduction: deterministic, no atomics.
+     forward  y = x W:      a = x, sam = I, sak = 1;   b = W, sbk = J, sbn = 1
+     input    dx = dy W^T:  a = dy, sam = J, sak = 1;  b = W, sbk = 1, sbn = J
+     weight   dW = x^T dy:  a = x, sam = 1, sak = I;   b = dy, sbk = J, sbn = 1, colsum = db */
+size_t sae_gemm_f32_workspace_bytes(int32_t M, int32_t N, int32_t K);
+int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, int64_t sam,
+                 int64_t sak, const float* b, int64_t sbk, int64_t sbn, const float* bias, float* c,
+                 int64_t ldc, float* colsum, int32_t accumulate, void* workspace);
 /* fp32 Dense kernel w [K][N] -> bf16 w16 [K][N] and/or its transpose wt16 [N][K] (either may
    be NULL): the compute-dtype casts of Flax Dense (kernel cast to dtype). */
 int sae_weight_cast(void* stream, int32_t K, int32_t N, const float* w, void* w16, void* wt16);

@@ -23,6 +23,7 @@
 #include "gemm_dw.h"
 #include "gemm_nt.h"
 #include "gemm8.h"
+#include "gemm_f32.h"
 #include "loss.h"
 #include "tokens.h"
 #include "patch.h"
@@ -550,15 +551,54 @@ static int device_cus() {
   return cus[dev];
 }
 
-// one persistent gemm8 launch (256 x BN tiles, one 8-wave workgroup per CU)
+// tile height of a gemm8 / gemm8x launch: 224 where 256-row tiles quantize worse onto the CUs --
+// cost = rounds of tiles over the CUs x rows per tile (M = 25,216 into 384 features: 198 tiles of
+// 256 rows, one round on 256 CUs with 58 idle, vs 226 of 224 rows; M = 18,464 into 768: 219 vs 249)
+static int g8_pick_bm(int M, int N, int BN) {
+#ifdef SAE_DEV_KNOBS
+  if (dev_knob("SAE_NT_BM256")) return 256;
+#endif
+  const long long G = device_cus(), tn = (N + BN - 1) / BN;
+  auto cost = [&](int bm) { return ((((long long)M + bm - 1) / bm * tn + G - 1) / G) * bm; };
+  return cost(224) < cost(256) ? 224 : 256;
+}
+
+// one persistent gemm8 launch (BM x BN tiles, one 8-wave workgroup per CU)
+template <int EPI, int BN, int BK, int NS, int BM>
+static int g8_launch_bm(const NtArgs& g, hipStream_t st) {
+  constexpr int lds = g8_lds_bytes<BN, BK, NS>();
+  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>, lds)) return rc;
+  const long long tiles = (long long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const long long grid = std::min<long long>(tiles, device_cus());
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  return 0;
+}
 template <int EPI, int BN, int BK, int NS>
 static int g8_launch(const NtArgs& g, hipStream_t st) {
-  constexpr int lds = g8_lds_bytes<BN, BK, NS>();
-  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS>, lds)) return rc;
-  const long long tiles = (long long)((g.M + 255) / 256) * ((g.N + BN - 1) / BN);
-  const long long grid = std::min<long long>(tiles, device_cus());
-  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  return g8_pick_bm(g.M, g.N, BN) == 224 ? g8_launch_bm<EPI, BN, BK, NS, 224>(g, st)
+                                         : g8_launch_bm<EPI, BN, BK, NS, 256>(g, st);
+}
+
+// one gemm8x launch (BM x BN tiles, ping-pong wave groups, one tile per workgroup)
+template <int EPI, int BN, int BM>
+static int g8x_launch_bm(const NtArgs& g, hipStream_t st) {
+  constexpr int lds = g8x_lds_bytes<BN, BM>();
+  if (int rc = lds_attr((const void*)gemm8x_nt_kernel<EPI, BN, true, BM>, lds)) return rc;
+  const long long tiles = (long long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm8x_nt_kernel<EPI, BN, true, BM>), dim3((unsigned)tiles), dim3(512), lds, st, g);
   return 0;
+}
+template <int EPI, int BN>
+static int g8x_launch(const NtArgs& g, hipStream_t st) {
+  return g8_pick_bm(g.M, g.N, BN) == 224 ? g8x_launch_bm<EPI, BN, 224>(g, st) : g8x_launch_bm<EPI, BN, 256>(g, st);
+}
+
+// the 768-feature outputs at reduction depth >= 768 (ViT-B output projection, QKV input gradient,
+// FF Dense_1 forward, Dense_0 input gradient): the ping-pong 256 x 256 kernel, 0.90-0.98 of the
+// library there (profiles/r04i_g8probe.txt: 1,086-1,132 vs 1,180-1,265 TF/s at K 2,304 / 3,072,
+// 820 vs 833 at K 768), so that no library GEMM runs in the ViT-B step
+static bool g8x_route(int M, int N, int K, int epilogue) {
+  return epilogue != SAE_EPI_DGELU && N == 768 && K >= 768 && K % 64 == 0 && M >= 4096;
 }
 
 // gemm8 (gemm8.h) or the 128-row sae_gemm_nt: tools/probe/gemm8_probe.py, profiles/r04c_g8probe.txt --
@@ -1079,6 +1119,84 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
   return check_launch("gemm_dw_reduce");
 }
 
+// ------------------------------------------------------------------ fp32 projections
+// split-K plan: more splits only while the output tiles leave the chip idle and each split keeps
+// >= 1,024 of depth (the weight gradients: K = the token count); independent of `colsum` so the
+// workspace bound holds for both
+static void f32_plan(int M, int N, int K, int* S, int* kchunk) {
+  const int tiles = ((M + kF32T - 1) / kF32T) * ((N + kF32T - 1) / kF32T);
+  int s = 1;
+  if (tiles < 256 && K >= 2048) s = std::min((512 + tiles - 1) / tiles, K / 1024);
+  s = std::max(1, std::min(s, 64));
+  int c = (K + s - 1) / s;
+  c = (c + kF32K - 1) / kF32K * kF32K;
+  *kchunk = c;
+  *S = (K + c - 1) / c;
+}
+
+size_t sae_gemm_f32_workspace_bytes(int32_t M, int32_t N, int32_t K) {
+  if (M < 1 || N < 1 || K < 1) return 0;
+  int S, c;
+  f32_plan(M, N, K, &S, &c);
+  return S > 1 ? (size_t)S * (M + 1) * N * 4 : 0;
+}
+
+int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, int64_t sam, int64_t sak,
+                 const float* b, int64_t sbk, int64_t sbn, const float* bias, float* c, int64_t ldc,
+                 float* colsum, int32_t accumulate, void* workspace) {
+  if (M < 1 || N < 1 || K < 1) return fail(SAE_EINVAL, "gemm_f32: M/N/K must be >= 1 (got %d/%d/%d)", M, N, K);
+  if (!a || !b || !c) return fail(SAE_EINVAL, "gemm_f32: a, b and c must be non-NULL");
+  const bool ak = sak == 1, bk = sbk == 1;
+  if (ak ? (sam < K || sam % 4 || K % 4) : (sam != 1 || sak < M || sak % 4 || M % 4))
+    return fail(SAE_EUNSUPPORTED, "gemm_f32: A needs unit stride along k (sam >= K, K and sam multiples of 4) "
+                "or along m (sak >= M, M and sak multiples of 4); got sam %lld sak %lld", (long long)sam,
+                (long long)sak);
+  if (bk ? (sbn < K || sbn % 4 || K % 4) : (sbn != 1 || sbk < N || sbk % 4 || N % 4))
+    return fail(SAE_EUNSUPPORTED, "gemm_f32: B needs unit stride along k (sbn >= K, K and sbn multiples of 4) "
+                "or along n (sbk >= N, N and sbk multiples of 4); got sbk %lld sbn %lld", (long long)sbk,
+                (long long)sbn);
+  if (ldc < N) return fail(SAE_EINVAL, "gemm_f32: ldc (%lld) < N (%d)", (long long)ldc, N);
+  if (!aligned16(a) || !aligned16(b)) return fail(SAE_EINVAL, "gemm_f32: a and b must be 16-byte aligned");
+  F32Args g;
+  memset(&g, 0, sizeof g);
+  g.a = a;
+  g.b = b;
+  g.bias = bias;
+  g.c = c;
+  g.colsum = colsum;
+  g.sam = sam;
+  g.sak = sak;
+  g.sbk = sbk;
+  g.sbn = sbn;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.accumulate = accumulate;
+  f32_plan(M, N, K, &g.S, &g.kchunk);
+  if (g.S > 1) {
+    if (!workspace || !aligned16(workspace))
+      return fail(SAE_EINVAL, "gemm_f32: this shape splits K: pass sae_gemm_f32_workspace_bytes() of 16-byte "
+                  "aligned workspace");
+    g.part = reinterpret_cast<float*>(workspace);
+  }
+  const int Mx = M + (colsum ? 1 : 0);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((Mx + kF32T - 1) / kF32T, (N + kF32T - 1) / kF32T, g.S);
+  if (ak && bk) hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, st, g);
+  else if (ak) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, st, g);
+  else if (bk) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, st, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, st, g);
+  if (int rc = check_launch("gemm_f32")) return rc;
+  if (g.S > 1) {
+    const long long n = (long long)Mx * N;
+    const unsigned rb = (unsigned)std::min<long long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3(rb), dim3(256), 0, st, g);
+    return check_launch("gemm_f32_reduce");
+  }
+  return 0;
+}
+
 // ------------------------------------------------------------ forward / input-gradient GEMMs
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
                 int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
@@ -1115,6 +1233,15 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   g.ldc = ldc;
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
+  if (g8x_route(M, N, K, epilogue)
+#ifdef SAE_DEV_KNOBS
+      && !dev_knob("SAE_NT_NO_G8")
+#endif
+  ) {
+    const int rc = epilogue == SAE_EPI_NONE ? g8x_launch<kEpiNone, 256>(g, st) : g8x_launch<kEpiGelu, 256>(g, st);
+    if (rc) return rc;
+    return check_launch("gemm8x_nt");
+  }
   if (g8_route(M, N, K, epilogue)
 #ifdef SAE_DEV_KNOBS
       && !dev_knob("SAE_NT_NO_G8")

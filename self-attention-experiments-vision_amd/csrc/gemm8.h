@@ -82,9 +82,12 @@ template <int BK> __device__ __forceinline__ int g8_swz(int r) {
   else return (r >> 1) & 7;
 }
 
-template <int BN> struct G8Cfg {
-  static constexpr int BM = 256;
-  static constexpr int WM = 128, WN = BN / 4;     // wave tile (2 x 4 waves)
+// BM: tile rows (256, or 224 where 256-row tiles leave CUs idle: M = 25,216 into 384 features is
+// 198 tiles of 256 x 192 on 256 CUs but 226 of 224 x 192; the A image keeps 256 rows, the rows past
+// BM read as zero through the descriptor's range check -- no memory traffic)
+template <int BN, int BM = 256> struct G8Cfg {
+  static_assert(BM % 32 == 0 && BM <= 256, "tile rows");
+  static constexpr int WM = BM / 2, WN = BN / 4;  // wave tile (2 x 4 waves)
   static constexpr int MT = WM / 16, NT = WN / 16; // 16 x 16 accumulator tiles per wave
 };
 
@@ -102,10 +105,10 @@ template <int BN, int BK, int NS> constexpr int g8_lds_bytes() {
 // per-wave scratch, 32 rows at a time: 16-byte row-segment stores), so neither the prologue's load
 // latency nor the epilogue's stores stall the ring.
 // MODE (probe builds only): 0 = the kernel; 1 = no global stores; 2 = no MFMAs (staging only)
-template <int EPI, int BN, int BK, int NS, int MODE = 0>
+template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256>
 __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using C = G8Cfg<BN>;
+  using C = G8Cfg<BN, BM>;
   constexpr int RB = BK * 2;                  // image row bytes
   constexpr int CPR = BK / 8;                 // 16-byte chunks per row
   constexpr int RPP = 64 / CPR;               // rows per 1-KiB piece
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   constexpr int PBX = PBT % 8;                // waves with PB0 pieces (0: every wave has PB1)
 
   const int tn = (a.N + BN - 1) / BN;
-  const int ntiles = ((a.M + 255) / 256) * tn;
+  const int ntiles = ((a.M + BM - 1) / BM) * tn;
   const int G = gridDim.x;
   const int b0 = xcd_remap(blockIdx.x, G);
   const int myt = (ntiles - b0 + G - 1) / G;  // tiles of this workgroup: b0, b0 + G, ...
@@ -151,8 +154,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   g8_u32x4 ra, rb;
   auto set_issue_tile = [&](int it) {
     const int t = b0 + it * G;
-    const int m0 = (t / tn) * 256, n0 = (t % tn) * BN;
-    ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(256, a.M - m0), a.lda);
+    const int m0 = (t / tn) * BM, n0 = (t % tn) * BN;
+    ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(BM, a.M - m0), a.lda);
     rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
   };
   auto issue_next = [&]() {
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   // fragment read offsets: row base + (lane & 15), chunk 4 kk + (lane >> 4)
   const int fr = lane & 15, fg = lane >> 4;
   const int sw = g8_swz<BK>(fr);   // rows are 16-aligned + fr: the swizzle depends on fr only
-  const char* pa0 = smem + (128 * wr + fr) * RB;
+  const char* pa0 = smem + (C::WM * wr + fr) * RB;   // WM a multiple of 16: the swizzle stays g8_swz(fr)
   const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB;
   constexpr int SRB = C::WN * 2 + 16;             // scratch row bytes (wave tile row + pad)
   constexpr int SCH = C::WN / 8;                  // 16-byte chunks per tile row
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
     // m = 128 wr + 16 i + fr (tile-relative); through the wave's scratch 32 rows at a time
     const int t = b0 + cti * G;
     ++cti;
-    const int m0 = (t / tn) * 256 + 128 * wr, nw = (t % tn) * BN + C::WN * wc;
+    const int m0 = (t / tn) * BM + C::WM * wr, nw = (t % tn) * BN + C::WN * wc;
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
     f32x4 bv[C::NT];
 #pragma unroll
@@ -242,10 +245,11 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
                                                         : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int ip = 0; ip < C::MT / 2; ++ip) {
+    for (int ip = 0; ip < (C::MT + 1) / 2; ++ip) {
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int i = 2 * ip + h2;
+        if (i >= C::MT) break;   // odd MT: the last group holds 16 rows
 #pragma unroll
         for (int j = 0; j < C::NT; ++j) {
           const bf16x4 v = {(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
@@ -261,6 +265,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
         const int rr = id / SCH, c = id % SCH;
         const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * SRB + 16 * c);
         const int m = m0 + 32 * ip + rr, n = nw + 8 * c;
+        if (32 * ip + rr >= C::WM) continue;
         if (MODE == 1) {
           if (raw.x == 0x7fc07fc0u && raw.y == 0x12345678u) a.c[0] = (__bf16)1.f;   // keep the reads
         } else if (m < a.M && n < a.N) {
@@ -282,6 +287,186 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
     }
   }
   if (w >= 4) __builtin_amdgcn_s_setprio(0);
+}
+
+}  // namespace sae
+
+namespace sae {
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong variant (long reductions): one 256 x BN tile per workgroup (not persistent), K-tiles of
+// 32 through a 4-deep LDS ring (K-tile t + 2 issued while t computes), and the two wave groups
+// -- waves 0-3 (tile rows 0-127) and 4-7 (rows 128-255) -- one barrier apart: each K-tile is two
+// phases per group, a load segment (LDS-DMA issue, fragment reads, the stage wait) and an MFMA
+// segment (16 MFMAs at s_setprio 1), so on every SIMD one wave's load segment runs beside its
+// partner's MFMAs (cdna_hip_programming.md section 5, the 8-phase template; MI355X_MICROARCH.md,
+// two waves per SIMD).  RAW: a stage is waited for (counted vmcnt) in the load segment of the
+// phase before the one that first reads it, and every group passes a barrier in between; WAR:
+// K-tile t + 2 overwrites the buffer of t - 2, read four phases (eight barriers) earlier.
+// BAL: the A pieces of K-tile t + 2 go out in phase 0, its B pieces in phase 1 after that phase's
+// wait (both load segments carry DMA; the wait counts only the two A pieces, for every wave)
+template <int EPI, int BN, bool BAL = false, int BM = 256>
+__global__ __launch_bounds__(512, 1) void gemm8x_nt_kernel(NtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using C = G8Cfg<BN, BM>;
+  static_assert(C::MT > 4 && C::MT <= 8, "phase 0 computes rows 0-63 of a wave tile, phase 1 the rest");
+  static_assert(C::WM * (C::WN / 8) % 64 == 0, "epilogue: whole 64-lane store rounds");
+  constexpr int RB = 64;                       // image row bytes (BK = 32)
+  constexpr int IMGA = 256 * RB, STAGE = (256 + BN) * RB;
+  constexpr int PBT = BN / 16;                 // B pieces per stage (16 rows per piece)
+  constexpr int PB0 = (PBT + 7) / 8, PB1 = PBT / 8, PBX = PBT % 8;
+
+  const int tn = (a.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / tn) * BM, n0 = (bid % tn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, wc = w & 3;
+  const g8_u32x4 ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(BM, a.M - m0), a.lda);
+  const g8_u32x4 rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
+  const unsigned lbase = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+  const int prow = lane >> 2, pc = lane & 3;
+  unsigned goa[2], gob[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (w + 8 * i) + prow;
+    goa[i] = (unsigned)(((long long)row * a.lda + 8 * (pc ^ g8_swz<32>(row))) * 2);
+    gob[i] = (unsigned)(((long long)row * a.ldb + 8 * (pc ^ g8_swz<32>(row))) * 2);
+  }
+  const bool bx = PBX == 0 || w < PBX;
+  auto issue_a = [&](int kt) __attribute__((always_inline)) {
+    const unsigned ko = (unsigned)kt * RB;
+    const unsigned lb = lbase + (unsigned)((kt & 3) * STAGE);
+    g8_dma2(ra, goa[0] + ko, goa[1] + ko, lb + 1024u * w, lb + 1024u * (w + 8));
+  };
+  auto issue_b = [&](int kt) __attribute__((always_inline)) {
+    const unsigned ko = (unsigned)kt * RB;
+    const unsigned lb = lbase + (unsigned)((kt & 3) * STAGE);
+    if (PB0 == 2 && bx)
+      g8_dma2(rb, gob[0] + ko, gob[1] + ko, lb + IMGA + 1024u * w, lb + IMGA + 1024u * (w + 8));
+    else if (PB0 >= 1 && (PB1 >= 1 || bx))
+      g8_dma1(rb, gob[0] + ko, lb + IMGA + 1024u * w);
+  };
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    issue_a(kt);
+    issue_b(kt);
+  };
+  const int fr = lane & 15, fg = lane >> 4;
+  const int co = 16 * (fg ^ g8_swz<32>(fr));
+  const char* pa0 = smem + (C::WM * grp + fr) * RB + co;
+  const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB + co;
+  f32x4 acc[C::MT][C::NT];
+#pragma unroll
+  for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = a.K / 32;
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) {
+    if (bx) g8_wait_barrier<2 + PB0>(); else g8_wait_barrier<2 + PB1>();
+  } else {
+    g8_wait_barrier<0>();
+  }
+  if (grp == 1) asm volatile("s_barrier" ::: "memory");   // the stagger
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* ia = pa0 + (kt & 3) * STAGE;
+    const char* ib = pb0 + (kt & 3) * STAGE;
+    // ---- phase 0: read B and the first half of A, issue K-tile kt + 2 (BAL: its A pieces)
+    bf16x8 bf[C::NT], af[4];
+#pragma unroll
+    for (int j = 0; j < C::NT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(ib + 16 * j * RB);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * i * RB);
+    if (kt + 2 < nkt) {
+      if constexpr (BAL) issue_a(kt + 2);
+      else issue(kt + 2);
+    }
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 1: read the second half of A; K-tile kt + 1 must have landed before the next
+    // phase's reads (BAL: then the B pieces of kt + 2)
+#pragma unroll
+    for (int i = 0; i < C::MT - 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * (4 + i) * RB);
+    if (kt + 1 < nkt) {
+      if (kt + 2 < nkt) {
+        if constexpr (BAL) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (bx) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + PB0) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + PB1) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    if constexpr (BAL)
+      if (kt + 2 < nkt) issue_b(kt + 2);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < C::MT - 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NT; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (grp == 0) asm volatile("s_barrier" ::: "memory");   // balance the stagger
+  asm volatile("s_barrier" ::: "memory");                  // every wave done with the ring
+
+  // ---- epilogue through a per-wave scratch (the ring is free): acc[i][j] = D[n][m]
+  constexpr int SRB = C::WN * 2 + 16, SCH = C::WN / 8;
+  char* scratch = smem + w * (C::WM * SRB);
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  const int nw = n0 + C::WN * wc;
+  f32x4 bv[C::NT];
+#pragma unroll
+  for (int j = 0; j < C::NT; ++j) {
+    const int n = nw + 16 * j + 4 * fg;
+    bv[j] = (a.bias && n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NT; ++j) {
+      const bf16x4 v = {(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
+                        (__bf16)(acc[i][j][2] + bv[j][2]), (__bf16)(acc[i][j][3] + bv[j][3])};
+      *reinterpret_cast<bf16x4*>(scratch + (16 * i + fr) * SRB + 2 * (16 * j + 4 * fg)) = v;
+    }
+  __builtin_amdgcn_wave_barrier();
+  const int mw = m0 + C::WM * grp;
+#pragma unroll 4
+  for (int it = 0; it < C::WM * SCH / 64; ++it) {
+    const int id = it * 64 + lane;
+    const int rr = id / SCH, c = id % SCH;
+    const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * SRB + 16 * c);
+    const int m = mw + rr, n = nw + 8 * c;
+    if (m < a.M && n < a.N) {
+      if constexpr (EPI == kEpiNone) {
+        *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
+      } else {
+        *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
+        const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
+        *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+      }
+    }
+  }
+}
+
+template <int BN, int BM = 256> constexpr int g8x_lds_bytes() {
+  constexpr int ring = 4 * (256 + BN) * 64, scratch = 8 * (BM / 2) * (BN / 4 * 2 + 16);
+  return ring > scratch ? ring : scratch;
 }
 
 }  // namespace sae

@@ -613,6 +613,50 @@ def gemm_dw(x2: torch.Tensor, dy2: torch.Tensor, dw: torch.Tensor, db: Optional[
         _TIMER.end(tok, (M, I, J))
 
 
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
+             accumulate: bool = False) -> torch.Tensor:
+    """``a @ b (+ bias)`` in exact fp32 through ``sae_gemm_f32`` (f32-input MFMA).  ``a`` [M, K] and
+    ``b`` [K, N] are fp32 views with a unit stride along one dimension each (a transposed view is
+    read in place: ``x.t()`` for a weight gradient, ``w.t()`` for an input gradient).  ``colsum``
+    (fp32 [N]) also receives the column sums of ``b`` (a bias gradient); ``accumulate`` adds into
+    ``out`` / ``colsum``."""
+    lib = L.load()
+    _require_gpu(a, b)
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K:
+        raise ValueError(f"gemm_f32: a {tuple(a.shape)} and b {tuple(b.shape)} disagree on K")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    elif out.dtype != torch.float32 or tuple(out.shape) != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm_f32: out must be fp32 [{M}, {N}] with unit column stride")
+    if bias is not None:
+        bias = bias.float().contiguous()
+    nbytes = lib.sae_gemm_f32_workspace_bytes(M, N, K)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device) if nbytes else None
+    tok = _TIMER.begin("gemm_f32") if _TIMER is not None else None
+    L.check(lib.sae_gemm_f32(_stream(a), M, N, K, _ptr(a), a.stride(0), a.stride(1), _ptr(b), b.stride(0),
+                             b.stride(1), _ptr(bias), _ptr(out), out.stride(0), _ptr(colsum), int(accumulate),
+                             _ptr(ws)))
+    if tok is not None:
+        _TIMER.end(tok, (M, K, N))
+    return out
+
+
+def _f32_operand_ok(t: torch.Tensor) -> bool:
+    """A view sae_gemm_f32 reads in place: fp32, unit stride along one dim, 16-byte aligned, the
+    other stride and the contiguous extent multiples of 4."""
+    if not t.is_cuda or t.dtype != torch.float32 or t.dim() != 2 or t.data_ptr() % 16:
+        return False
+    r, c = t.shape
+    if t.stride(1) == 1:
+        return t.stride(0) % 4 == 0 and c % 4 == 0 and t.stride(0) >= c
+    if t.stride(0) == 1:
+        return t.stride(1) % 4 == 0 and r % 4 == 0 and t.stride(1) >= r
+    return False
+
+
 def _dw_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
     return (x2.is_cuda and x2.dtype == dy2.dtype == torch.bfloat16 and x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0
             and x2.stride(1) == 1 and dy2.stride(1) == 1 and x2.stride(0) % 8 == 0 and dy2.stride(0) % 8 == 0
@@ -768,7 +812,9 @@ class _Dense(torch.autograd.Function):
         J = sum(w.shape[1] for w in ws)
         x2 = x.to(dt).reshape(-1, I)
         wd, wt = _cast(ws, dt)
-        if wt is not None and use_gemm_nt(I, J) and _nt_ok(x2, J):
+        if dt == torch.float32 and _f32_operand_ok(x2) and _f32_operand_ok(wd):
+            y = gemm_f32(x2, wd, b)                       # exact fp32 on the f32 MFMA, bias in the epilogue
+        elif wt is not None and use_gemm_nt(I, J) and _nt_ok(x2, J):
             y = gemm_nt(x2, wt, b)                        # bias in the epilogue
         else:
             # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
@@ -787,6 +833,8 @@ class _Dense(torch.autograd.Function):
         dy2 = dy.reshape(-1, J)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
             dy2 = dy2.contiguous()
+        if wd.dtype == torch.float32 and _f32_operand_ok(dy2) and _f32_operand_ok(x2) and _f32_operand_ok(wd):
+            return _Dense._backward_f32(ctx, x2, wd, dy2)
         if use_gemm_nt(J, I) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
         else:
@@ -829,6 +877,26 @@ class _Dense(torch.autograd.Function):
             dws.append(dw[:, col:col + n].to(wdt))
             col += n
         return (dx, db, None, *dws)
+
+    @staticmethod
+    def _backward_f32(ctx, x2, wd, dy2):
+        """fp32 compute dtype: dX = dY W^T, then per column block dW_k = X^T dY[:, block] with that
+        block's db slice as the ones-row column sum, all on sae_gemm_f32; sinks written in place."""
+        I, J = wd.shape
+        dx = gemm_f32(dy2, wd.t()).view(ctx.xshape).to(ctx.xdtype)
+        sb = ctx.sink_b
+        db = _claim(sb) if sb is not None else (
+            torch.empty((J,), dtype=torch.float32, device=x2.device) if ctx.has_b else None)
+        dws, col = [], 0
+        for (n, wdt), sw in zip(ctx.wmeta, ctx.sinks_w):
+            dst = _claim(sw) if sw is not None else torch.empty((I, n), dtype=torch.float32, device=x2.device)
+            dyb = dy2[:, col:col + n]
+            if not _f32_operand_ok(dyb):
+                dyb = dyb.contiguous()
+            gemm_f32(x2.t(), dyb, out=dst, colsum=db[col:col + n] if db is not None else None)
+            dws.append(None if sw is not None else dst.to(wdt))
+            col += n
+        return (dx, None if sb is not None else db, None, *dws)
 
 
 def dense(x: torch.Tensor, w, b: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
@@ -936,6 +1004,7 @@ EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 # same-box A/B (profiles/r03o_vitb_route_ab.txt): every GEMM on sae_gemm_nt 19.0 ms/step, K <= 768
 # on it 18.0, this split 17.8.  GEMM_NT_ALL = True routes everything to sae_gemm_nt (A/B runs).
 GEMM_NT_ALL = False
+GEMM_LIB_WIDE = 0   # A/B switch (tools/ab_knob.py ops.GEMM_LIB_WIDE=v): 1 = round-3 routing (library for K >= 768), 2 = library for the N = 768 outputs only
 GEMM_NT_MAX_K = 512
 GEMM_NT_NARROW_N = 384
 GEMM_NT_NARROW_MAX_K = 1536
@@ -943,11 +1012,18 @@ GEMM_NT_NARROW_MAX_K = 1536
 
 def use_gemm_nt(K: int, N: int) -> bool:
     """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt.
-    Round 4: the wide K = 768 outputs (ViT-B QKV forward, N 2304; FF Dense_0, N 3072) go to it as
-    well -- the C-ABI runs them on the 256-row persistent gemm8 kernel, level with the library
-    (profiles/r04c_g8probe.txt); the 768-feature outputs at K >= 768 stay on the library."""
-    return (GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
-            or (K == 768 and N % 192 == 0 and 1152 <= N <= 3072))
+    Round 4: the ViT-B shapes go to it as well -- the wide K = 768 outputs (QKV forward, N 2304;
+    FF Dense_0, N 3072) run on the persistent 256-row gemm8 kernel, the 768-feature outputs at
+    K >= 768 (output projection, QKV / Dense_0 input gradients, Dense_1 forward) on the ping-pong
+    gemm8x kernel: 0.90-1.0 of the library there (profiles/r04c_g8probe.txt, r04i_g8probe.txt), and
+    no library GEMM left on the ViT-B@384 path."""
+    base = GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
+    if GEMM_LIB_WIDE == 1:
+        return base
+    wide_in = K == 768 and N % 192 == 0 and 1152 <= N <= 3072
+    if GEMM_LIB_WIDE == 2:
+        return base or wide_in
+    return base or wide_in or (N == 768 and K >= 768 and K % 64 == 0)
 
 
 def _nt_ok(a2: torch.Tensor, N: int) -> bool:
@@ -1017,8 +1093,8 @@ class _FFBlock(torch.autograd.Function):
         a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
         # Dense_1 forward is a plain GEMM + bias: sae_gemm_nt up to K = hidden 1536 (DeiT-S: 42 vs 44 us for
         # the library), the library beyond (ViT-B hidden 3072: 82 vs 100 us, profiles/r01_gemm_probe_v13.txt)
-        y = gemm_nt(a, w1t, b1) if Hd <= FF_NT_MAX_HIDDEN else torch.addmm(b1.to(a.dtype), a, w1p) if b1 is not None \
-            else a @ w1p
+        y = gemm_nt(a, w1t, b1) if Hd <= FF_NT_MAX_HIDDEN or use_gemm_nt(Hd, w1t.shape[0]) else \
+            torch.addmm(b1.to(a.dtype), a, w1p) if b1 is not None else a @ w1p
         ctx.save_for_backward(x2, h, a, w0p, w1p)
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
         ctx.sinks = [_sink(t) for t in (w0, b0, w1, b1)]

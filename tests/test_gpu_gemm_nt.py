@@ -225,12 +225,14 @@ def test_gemm_nt_odd_stages_repeatable(dev, K):
 # K = 768 forwards to): one tile per workgroup (25216 x 384: 198 tiles), several per workgroup
 # (70000 x 384: 548 tiles; 18464 x 2304: 1,152 tiles), ragged last row block (5000, 70000, 18464)
 G8_SHAPES = [(25216, 384, 384), (25216, 1152, 384), (25216, 1536, 384), (5000, 384, 384), (70000, 384, 384),
-             (18464, 768, 2304)]
+             (18464, 768, 2304),
+             # gemm8x (ping-pong wave groups, 256 x 256 tiles): the ViT-B 768-feature outputs
+             (18464, 3072, 768), (18464, 768, 768), (5000, 2304, 768)]
 
 
 @pytest.mark.parametrize("M,K,N", G8_SHAPES)
 def test_gemm8_plain_repeatable(dev, M, K, N):
-    """gemm8: against the float64 product (bias in the first K-tile's MFMA C operand) and bit-equal
+    """gemm8 / gemm8x: against the float64 product (bias in the first K-tile's MFMA C operand) and bit-equal
     over reruns (a stage read before its LDS-DMA landed shows up as run-to-run differences)."""
     import sae_vision_amd.ops as ops
     a, bt, b = _inputs(dev, M, K, N, 3 * M + K)

@@ -6,6 +6,7 @@ interleaved over rounds; median ms/step.
 
     SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so python tools/ab_knob.py KNOB=v1 [KNOB=v2 ...] [--model m]
     e.g. python tools/ab_knob.py SAE_NT_NO_G8=1 SAE_NT_NO_G8=0
+         python tools/ab_knob.py ops.GEMM_LIB_WIDE=1 ops.GEMM_LIB_WIDE=0   (module flags of ops)
 """
 import argparse
 import copy
@@ -39,12 +40,20 @@ def main():
     images = torch.randn(a.batch, a.img_size, a.img_size, 3, device=dev, generator=g)
     labels = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
     steps = {}
+    from sae_vision_amd import ops
     for v in a.variants:
         k, val = v.split("=")
-        os.environ[k] = val
+        if k.startswith("ops."):   # a module flag of ops (routing decisions are taken at capture)
+            old = getattr(ops, k[4:])
+            setattr(ops, k[4:], type(old)(int(val)) if isinstance(old, bool) else type(old)(val))
+        else:
+            os.environ[k] = val
         s = train.TrainStep(copy.deepcopy(base), global_batch=a.batch, device=dev, graph=True)
         s(images, labels)        # capture under this knob
-        os.environ.pop(k)
+        if k.startswith("ops."):
+            setattr(ops, k[4:], old)
+        else:
+            os.environ.pop(k)
         steps[v] = s
     torch.cuda.synchronize()
     res = {v: [] for v in steps}

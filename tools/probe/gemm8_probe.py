@@ -20,6 +20,8 @@ LIB.g8_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int
 # variant % 10: tile / stage depth / ring; variant >= 10: persistent grid of 256 workgroups
 NAMES = {0: "256x256 bk32 ns3", 1: "256x192 bk32 ns3", 2: "256x192 bk32 ns4", 3: "256x192 bk64 ns2",
          4: "256x128 bk32 ns4", 5: "256x128 bk64 ns2"}
+# 40-45: gemm8x ping-pong (43 = 256 x 256 BAL, 45 = 224 x 256 BAL); 50 / 51 / 53: persistent 224 x 256 bk32 ns3,
+# 192 x 192 bk64 ns2, 224 x 192 bk64 ns2 (tile heights that fill 256 CUs at M = 25,216 / 18,464)
 
 
 def bench(fn, iters=20):
