@@ -119,7 +119,7 @@ def cpu_baseline(model_name, seconds_budget=15.0):
             break
     dt = time.perf_counter() - t0
     out = {"value": round(n_img / dt, 3), "unit": "img/s", "cores": int(cores), "kind": "port",
-           "affinity_cpus": len(os.sched_getaffinity(0)),
+           "affinity_cpus": len(os.sched_getaffinity(0)), "cores_note": CORES_NOTE,
            "sample": f"{model_name} fp32 numpy train step (fwd+loss+bwd+AdamW), batch {bs} x {n_img // bs} steps, "
                      f"{dt:.1f} s"}
     # BASELINE configs[0]: DeiT-Tiny/16 forward + loss on a 224 px batch of 8, the CPU reference path
@@ -141,6 +141,13 @@ def cpu_baseline(model_name, seconds_budget=15.0):
     return out
 
 
+# why `cores` is below `affinity_cpus`: the GPU box gives one GPU's job a 16-CPU share of the host
+# (OMP_NUM_THREADS / MAX_JOBS are set to 16 there and worker pools must stay within it); the
+# affinity mask still lists every CPU of the 8-GPU machine, which the other GPUs' jobs use
+CORES_NOTE = ("threads = OMP_NUM_THREADS, the box's CPU share for one GPU (16 of the machine's CPUs; "
+              "affinity_cpus counts all of them, shared with the other GPUs' jobs)")
+
+
 def cpu_attention_baseline(seconds_budget=5.0, B=16, N=197, H=6, D=64):
     """SURVEY §8d's CPU baseline of metric (1): the unfused reference attention core (S and P
     materialised, softmax, AV; backward through dP / dS) as C + OpenMP over (batch, head), fp32
@@ -160,7 +167,8 @@ def cpu_attention_baseline(seconds_budget=5.0, B=16, N=197, H=6, D=64):
     dt = (time.perf_counter() - t0) / n
     f_fwd, f_bwd, _, _ = attn_work(B, N, N, H, D)
     return {"value": round((f_fwd + f_bwd) / dt / 1e12, 5), "unit": "TFLOP/s", "ms_per_call": round(dt * 1e3, 2),
-            "cores": attn_cpu.threads(), "affinity_cpus": len(os.sched_getaffinity(0)), "kind": "port",
+            "cores": attn_cpu.threads(), "affinity_cpus": len(os.sched_getaffinity(0)), "cores_note": CORES_NOTE,
+            "kind": "port",
             "sample": f"unfused fp32 attention core fwd+bwd (C + OpenMP, oracle/attn_cpu.c), B={B} N={N} H={H} "
                       f"D={D}, {n} calls"}
 
