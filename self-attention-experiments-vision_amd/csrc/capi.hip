@@ -24,6 +24,7 @@
 #include "gemm_nt.h"
 #include "gemm8.h"
 #include "gemm_f32.h"
+#include "gemm_dw8.h"
 #include "loss.h"
 #include "tokens.h"
 #include "patch.h"
@@ -528,6 +529,19 @@ static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hip
   return 0;
 }
 
+// the LDS-DMA form of the plain weight-gradient kernel (gemm_dw8.h)
+template <int NG>
+static int dw8_launch(const DwArgs& a, bool bias, long long grid, hipStream_t st) {
+  constexpr int lds = dw8_lds_bytes<NG>();
+  const void* fn = bias ? (const void*)gemm_dw8_kernel<true, NG> : (const void*)gemm_dw8_kernel<false, NG>;
+  if (int rc = lds_attr(fn, lds)) return rc;
+  if (bias)
+    hipLaunchKernelGGL((gemm_dw8_kernel<true, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+  else
+    hipLaunchKernelGGL((gemm_dw8_kernel<false, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+  return 0;
+}
+
 // one sae_gemm_nt launch: TM x 128 tiles, two LDS stage buffers of BK-deep A and B images
 template <int EPI, class AL>
 static int nt_launch(const NtArgs& g, long long grid, hipStream_t st) {
@@ -607,9 +621,13 @@ static bool g8x_route(int M, int N, int K, int epilogue) {
 // ViT-B forwards (QKV 2304 features 750 -> 850-900, FF Dense_0 + GELU 673-700 -> 715-729: level with
 // the library's 830-960); the 128-row kernel stays on the DeiT-S wide K = 384 outputs (a tie) and
 // the GELU' epilogue (gemm8 has none)
+// Round 4 (224-row tiles, g8_pick_bm): also the DeiT-S / CaiT wide K = 384 outputs -- QKV forward
+// 593 -> 647 TF/s, FF Dense_0 + GELU 546 -> 563, Dense_1 input gradient with GELU' 497 -> 509
+// (profiles/r04k_g8probe.txt, v53 vs rel)
 static bool g8_route(int M, int N, int K, int epilogue) {
-  if (epilogue == SAE_EPI_DGELU || N % 192 || K % 64 || K < 384 || M < 4096) return false;
-  return N == 384 || (K >= 768 && N >= 1152 && N <= 3072);
+  if (N % 192 || K % 64 || K < 384 || M < 4096 || N > 3072) return false;
+  if (epilogue == SAE_EPI_DGELU) return K == 384;
+  return N == 384 || K == 384 || (K >= 768 && N >= 1152);
 }
 
 extern "C" {
@@ -1107,7 +1125,14 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
   const size_t lds = NG * 4 * kDwK * 256;
   typedef DwRow<false> XR;
   typedef DwRow<true> YR;
-  if (NG == 2) {
+  bool dma = true;
+#ifdef SAE_DEV_KNOBS
+  dma = !dev_knob("SAE_DW_OLD");
+#endif
+  if (dma) {
+    if (int rc = NG == 2 ? dw8_launch<2>(a, db != nullptr, grid, st) : dw8_launch<1>(a, db != nullptr, grid, st))
+      return rc;
+  } else if (NG == 2) {
     if (int rc = dw_launch<XR, YR, 2>(a, db != nullptr, grid, lds, st)) return rc;
   } else {
     if (int rc = dw_launch<XR, YR, 1>(a, db != nullptr, grid, lds, st)) return rc;
@@ -1247,8 +1272,9 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
       && !dev_knob("SAE_NT_NO_G8")
 #endif
   ) {
-    const int rc = epilogue == SAE_EPI_NONE ? g8_launch<kEpiNone, 192, 64, 2>(g, st)
-                                            : g8_launch<kEpiGelu, 192, 64, 2>(g, st);
+    const int rc = epilogue == SAE_EPI_NONE   ? g8_launch<kEpiNone, 192, 64, 2>(g, st)
+                   : epilogue == SAE_EPI_GELU ? g8_launch<kEpiGelu, 192, 64, 2>(g, st)
+                                              : g8_launch<kEpiDGelu, 192, 64, 2>(g, st);
     if (rc) return rc;
     return check_launch("gemm8_nt");
   }
