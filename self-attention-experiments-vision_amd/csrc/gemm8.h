@@ -289,205 +289,6 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   if (w >= 4) __builtin_amdgcn_s_setprio(0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Deferred-epilogue variant of the persistent kernel (BK = 64, NS = 2).  In gemm8_nt_kernel a
-// tile's epilogue issues all its global stores at once, and the next stage's wait -- vmcnt counts
-// loads, stores and LDS-DMA together, in issue order -- then drains every one of them before the
-// next tile's MFMAs can start: at K = 384 a 256 x 192 tile's 96 KB of stores take about as long as
-// its MFMAs (per-CU share of the HBM write rate).  Here the finished tile is packed to bf16 in
-// registers (+bias) and its 32-row groups are stored one per stage while the next tile computes;
-// the wait for stage g + 1 counts the group stores issued after that stage's DMA (exactly SG
-// instructions when the group is whole, else 0: no under-count), so a group drains during one
-// stage of MFMAs instead of stalling the ring.
-template <int EPI, int BN, int BM = 256>
-__global__ __launch_bounds__(512, 1) void gemm8d_nt_kernel(NtArgs a) {
-  static_assert(EPI != kEpiDGelu, "the GELU' epilogue loads aux inside the epilogue: use gemm8_nt_kernel");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  using C = G8Cfg<BN, BM>;
-  constexpr int BK = 64, NS = 2;
-  constexpr int RB = BK * 2, CPR = BK / 8, RPP = 64 / CPR;
-  constexpr int IMGA = 256 * RB, STAGE = (256 + BN) * RB;
-  constexpr int PA = 256 / RPP / 8, PBT = BN / RPP;
-  constexpr int PB0 = (PBT + 7) / 8, PB1 = PBT / 8, PBX = PBT % 8;
-  constexpr int SRB = C::WN * 2 + 16, SCH = C::WN / 8;
-  constexpr int NGRP = (C::MT + 1) / 2;                         // 32-row groups per wave tile
-  constexpr int SG = (32 * SCH / 64) * (EPI == kEpiGelu ? 2 : 1); // store instructions per whole group
-  static_assert(32 * SCH % 64 == 0, "whole store rounds per group");
-
-  const int tn = (a.N + BN - 1) / BN;
-  const int ntiles = ((a.M + BM - 1) / BM) * tn;
-  const int G = gridDim.x;
-  const int b0 = xcd_remap(blockIdx.x, G);
-  const int myt = (ntiles - b0 + G - 1) / G;
-  const int nst = a.K / BK;
-  const int total = myt * nst;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 2, wc = w & 3;
-  const unsigned lbase = __builtin_amdgcn_readfirstlane(
-      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
-  const int prow = lane / CPR, pc = lane % CPR;
-  unsigned goa[PA], gob[PB0 > 0 ? PB0 : 1];
-#pragma unroll
-  for (int i = 0; i < PA; ++i) {
-    const int row = RPP * (w + 8 * i) + prow;
-    goa[i] = (unsigned)(((long long)row * a.lda + 8 * (pc ^ g8_swz<BK>(row))) * 2);
-  }
-#pragma unroll
-  for (int i = 0; i < (PB0 > 0 ? PB0 : 1); ++i) {
-    const int row = RPP * (w + 8 * i) + prow;
-    gob[i] = (unsigned)(((long long)row * a.ldb + 8 * (pc ^ g8_swz<BK>(row))) * 2);
-  }
-  const bool bx = PBX == 0 || w < PBX;
-  int iti = 0, ist = 0, ibuf = 0;
-  g8_u32x4 ra, rb;
-  auto set_issue_tile = [&](int it) __attribute__((always_inline)) {
-    const int t = b0 + it * G;
-    const int m0 = (t / tn) * BM, n0 = (t % tn) * BN;
-    ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(BM, a.M - m0), a.lda);
-    rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
-  };
-  auto issue_next = [&]() __attribute__((always_inline)) {
-    const unsigned ko = (unsigned)ist * RB;
-    const unsigned lb = lbase + (unsigned)(ibuf * STAGE);
-#pragma unroll
-    for (int i = 0; i < PA; i += 2) {
-      if (i + 1 < PA)
-        g8_dma2(ra, goa[i] + ko, goa[i + 1] + ko, lb + 1024u * (w + 8 * i), lb + 1024u * (w + 8 * (i + 1)));
-      else
-        g8_dma1(ra, goa[i] + ko, lb + 1024u * (w + 8 * i));
-    }
-#pragma unroll
-    for (int i = 0; i < PB0; ++i) {
-      if (i < PB1 || bx) g8_dma1(rb, gob[i] + ko, lb + IMGA + 1024u * (w + 8 * i));
-    }
-    ibuf ^= 1;
-    if (++ist == nst) {
-      ist = 0;
-      if (++iti < myt) set_issue_tile(iti);
-    }
-  };
-
-  f32x4 acc[C::MT][C::NT];
-#pragma unroll
-  for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-    for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-  bf16x4 pk[C::MT][C::NT];   // the finished tile, bf16 (+bias), waiting for its group stores
-  int pend = 0, pm0 = 0, pnw = 0;   // groups not yet stored; the packed tile's wave origin
-
-  const int fr = lane & 15, fg = lane >> 4;
-  const int sw = g8_swz<BK>(fr);
-  const char* pa0 = smem + (C::WM * wr + fr) * RB;
-  const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB;
-  char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN>();
-
-  // stores group ip of the packed tile; returns the number of store instructions it is sure to
-  // have issued (SG for a whole group, else 0)
-  auto store_group = [&](int ip) __attribute__((always_inline)) -> int {
-#pragma unroll
-    for (int q = 0; q < NGRP; ++q) {
-      if (q != ip) continue;
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int i = 2 * q + h2;
-        if (i >= C::MT) break;
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j)
-          *reinterpret_cast<bf16x4*>(scratch + (16 * h2 + fr) * SRB + 2 * (16 * j + 4 * fg)) = pk[i][j];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int it = 0; it < 32 * SCH / 64; ++it) {
-      const int id = it * 64 + lane;
-      const int rr = id / SCH, c = id % SCH;
-      const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * SRB + 16 * c);
-      const int m = pm0 + 32 * ip + rr, n = pnw + 8 * c;
-      if (32 * ip + rr < C::WM && m < a.M && n < a.N) {
-        if constexpr (EPI == kEpiNone) {
-          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
-        } else {
-          *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
-          const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
-          *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const bool whole = 32 * (ip + 1) <= C::WM && pm0 + 32 * (ip + 1) <= a.M && pnw + C::WN <= a.N;
-    return whole ? SG : 0;
-  };
-
-  if (myt > 0) set_issue_tile(0);
-  if (total > 0) issue_next();
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
-  int cur = 0, cst = 0, cti = 0, nprev = 0;
-  for (int g = 0; g < total; ++g) {
-    // stage g landed: everything older than the nprev group stores issued last iteration
-    if (nprev == SG) g8_wait_barrier<SG>(); else g8_wait_barrier<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    if (g + 1 < total) issue_next();
-    const char* ia = pa0 + cur * STAGE;
-    const char* ib = pb0 + cur * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int co = 16 * ((4 * kk + fg) ^ sw);
-      bf16x8 bf[C::NT], af[C::MT];
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(ib + 16 * j * RB + co);
-#pragma unroll
-      for (int i = 0; i < C::MT; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * i * RB + co);
-#pragma unroll
-      for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    cur ^= 1;
-    nprev = 0;
-    if (++cst == nst) {   // tile cti done: flush what is left of the previous one, pack this one
-      cst = 0;
-      bool irregular = false;
-      while (pend > 0) {
-        store_group(NGRP - pend);
-        --pend;
-        irregular = true;
-      }
-      const int t = b0 + cti * G;
-      ++cti;
-      pm0 = (t / tn) * BM + C::WM * wr;
-      pnw = (t % tn) * BN + C::WN * wc;
-      f32x4 bv[C::NT];
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j) {
-        const int n = pnw + 16 * j + 4 * fg;
-        bv[j] = (a.bias && n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) {
-          pk[i][j] = bf16x4{(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
-                            (__bf16)(acc[i][j][2] + bv[j][2]), (__bf16)(acc[i][j][3] + bv[j][3])};
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      pend = NGRP;
-      const int n = store_group(0);
-      --pend;
-      nprev = irregular ? 0 : n;
-    } else if (pend > 0) {
-      nprev = store_group(NGRP - pend);
-      --pend;
-    }
-  }
-  while (pend > 0) {
-    store_group(NGRP - pend);
-    --pend;
-  }
-  if (w >= 4) __builtin_amdgcn_s_setprio(0);
-}
-
 }  // namespace sae
 
 namespace sae {

@@ -35,18 +35,6 @@ static int launchx(const NtArgs& g, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-template <int EPI, int BM>
-static int launchd(const NtArgs& g, hipStream_t st) {
-  constexpr int lds = g8_lds_bytes<192, 64, 2>();
-  const void* fn = (const void*)gemm8d_nt_kernel<EPI, 192, BM>;
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return 2;
-  if (g.K % 64) return 4;
-  const long long tiles = (long long)((g.M + BM - 1) / BM) * ((g.N + 191) / 192);
-  const long long grid = std::min<long long>(tiles, 256);
-  hipLaunchKernelGGL((gemm8d_nt_kernel<EPI, 192, BM>), dim3((unsigned)grid), dim3(512), lds, st, g);
-  return hipGetLastError() == hipSuccess ? 0 : 3;
-}
-
 extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void* a, long long lda, const void* bt,
                       long long ldb, const float* bias, void* c, long long ldc, int epi, const void* aux,
                       long long ldaux, void* c2) {
@@ -72,8 +60,6 @@ extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void
   if (variant == 43) return epi == 0 ? launchx<kEpiNone, 256, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true>(g, st) : 5;
   if (variant == 44) return epi == 0 ? launchx<kEpiNone, 192, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 192, true>(g, st) : 5;
   if (variant == 45) return epi == 0 ? launchx<kEpiNone, 256, true, 224>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true, 224>(g, st) : 5;
-  if (variant == 60) return epi == 0 ? launchd<kEpiNone, 224>(g, st) : epi == 1 ? launchd<kEpiGelu, 224>(g, st) : 5;
-  if (variant == 61) return epi == 0 ? launchd<kEpiNone, 256>(g, st) : epi == 1 ? launchd<kEpiGelu, 256>(g, st) : 5;
   if (variant == 53) { g_persist = 256; return launch_epi<192, 64, 2, 224>(g, epi, st); }
   if (variant == 50) { g_persist = 256; return launch_epi<256, 32, 3, 224>(g, epi, st); }
   if (variant == 51) { g_persist = 256; return launch_epi<192, 64, 2, 192>(g, epi, st); }
