@@ -814,12 +814,13 @@ class _Dense(torch.autograd.Function):
         wd, wt = _cast(ws, dt)
         if dt == torch.float32 and _f32_operand_ok(x2) and _f32_operand_ok(wd):
             y = gemm_f32(x2, wd, b)                       # exact fp32 on the f32 MFMA, bias in the epilogue
-        elif wt is not None and use_gemm_nt(I, J) and _nt_ok(x2, J):
+        elif wt is not None and (use_gemm_nt(I, J) or x2.shape[0] <= SMALL_M) and _nt_ok(x2, J):
             y = gemm_nt(x2, wt, b)                        # bias in the epilogue
         else:
             # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
             y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
         ctx.save_for_backward(x2, wd)
+        ctx.wt = wt   # bf16 W^T [J, I] (the classifier head's input gradient reads it, below)
         ctx.has_b, ctx.xshape, ctx.xdtype = b is not None, x.shape, x.dtype
         ctx.wmeta = [(w.shape[1], w.dtype) for w in ws]
         ctx.sinks_w, ctx.sink_b = [_sink(w) for w in ws], _sink(b)
@@ -837,6 +838,14 @@ class _Dense(torch.autograd.Function):
             return _Dense._backward_f32(ctx, x2, wd, dy2)
         if use_gemm_nt(J, I) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
+        elif (wd.dtype == torch.bfloat16 and ctx.wt is not None and dy2.shape[0] <= SMALL_M and dy2.shape[0] % 8 == 0
+              and _dw_ok(dy2, ctx.wt)):
+            # K = J not a multiple of 64 (the classifier head: 1000 classes) -- the reduction runs
+            # over the ROWS of dY^T [J, M] and W^T [J, I], i.e. on the weight-gradient kernel:
+            # dx[m][i] = sum_j dY^T[j][m] W^T[j][i], fp32 then the activation dtype
+            dxf = torch.empty((dy2.shape[0], I), dtype=torch.float32, device=dy2.device)
+            gemm_dw(dy2.t().contiguous(), ctx.wt, dxf)
+            dx = dxf.view(ctx.xshape).to(ctx.xdtype)
         else:
             dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
         widths = [n for n, _ in ctx.wmeta]
@@ -1006,6 +1015,7 @@ EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 GEMM_NT_ALL = False
 GEMM_LIB_WIDE = 0   # A/B switch (tools/ab_knob.py ops.GEMM_LIB_WIDE=v): 1 = round-3 routing (library for K >= 768), 2 = library for the N = 768 outputs only
 GEMM_NT_MAX_K = 512
+SMALL_M = 4096   # Dense calls on at most this many rows (classifier heads, CLS-token projections) always take the HIP GEMMs
 GEMM_NT_NARROW_N = 384
 GEMM_NT_NARROW_MAX_K = 1536
 

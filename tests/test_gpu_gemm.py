@@ -86,6 +86,28 @@ def test_dense_grads_match_autograd(dev):
 
 
 
+@pytest.mark.parametrize("rows,C", [(32, 768), (128, 384)])
+def test_classifier_head_dense(dev, rows, C):
+    """The classifier head (C -> 1000 classes: K = 1000 is no multiple of 64 in the input gradient)
+    runs on the HIP kernels: forward on sae_gemm_nt (small-M rule), dX on the weight-gradient
+    kernel over the rows of dY^T / W^T; against float64 products of the same bf16 values."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(rows)
+    x = torch.randn(rows, C, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(C, 1000, device=dev, generator=g) * 0.05).requires_grad_()
+    b = torch.randn(1000, device=dev, generator=g).requires_grad_()
+    dy = torch.randn(rows, 1000, device=dev, generator=g).to(torch.bfloat16)
+    y = ops.dense(x, w, b, torch.bfloat16)
+    wd = w.detach().to(torch.bfloat16).double()
+    ref_y = x.detach().double() @ wd + b.detach().double()
+    assert float((y.double() - ref_y).abs().max() / ref_y.abs().max()) <= 2e-2
+    y.backward(dy)
+    ref_x = dy.double() @ wd.t()
+    assert float((x.grad.double() - ref_x).abs().max() / ref_x.abs().max()) <= 2e-2
+    ref_w = x.detach().double().t() @ dy.double()
+    assert float((w.grad.double() - ref_w).abs().max() / ref_w.abs().max()) <= 1e-5
+
+
 def test_gemm_dw_blocked_layout(dev):
     """sae_gemm_dw_blocked: dW in contiguous column blocks [J/jb, I, jb] equals the plain layout."""
     import sae_vision_amd.ops as ops
