@@ -192,6 +192,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB;
   constexpr int SRB = C::WN * 2 + 16;             // scratch row bytes (wave tile row + pad)
   constexpr int SCH = C::WN / 8;                  // 16-byte chunks per tile row
+  uint4 hv[EPI == kEpiDGelu ? (C::MT + 1) / 2 : 1][EPI == kEpiDGelu ? 32 * SCH / 64 : 1];   // GELU' aux tile
   char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN>();
 
   if (myt > 0) set_issue_tile(0);
@@ -212,6 +213,26 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
     }
     __builtin_amdgcn_sched_barrier(0);
     if (g + NS - 1 < total) issue_next();
+    if constexpr (EPI == kEpiDGelu) {
+      // GELU' epilogue: the tile's aux (h) chunks are loaded in one batch at the start of its last
+      // stage, so the epilogue's stores do not each wait out a dependent HBM round trip
+      if (cst == nst - 1) {
+        const int t = b0 + cti * G;
+        const int m0 = (t / tn) * BM + C::WM * wr, nw = (t % tn) * BN + C::WN * wc;
+#pragma unroll
+        for (int ip = 0; ip < (C::MT + 1) / 2; ++ip)
+#pragma unroll
+          for (int it = 0; it < 32 * SCH / 64; ++it) {
+            const int id = it * 64 + lane;
+            const int rr = id / SCH, c = id % SCH;
+            const int m = m0 + 32 * ip + rr, n = nw + 8 * c;
+            hv[ip][it] = (32 * ip + rr < C::WM && m < a.M && n < a.N)
+                             ? *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n)
+                             : uint4{0u, 0u, 0u, 0u};
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     const char* ia = pa0 + cur * STAGE;
     const char* ib = pb0 + cur * STAGE;
 #pragma unroll
@@ -276,9 +297,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
             const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
             *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
           } else {
-            const uint4 hv = *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n);
-            const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
-                             dgelu_bf2(raw.w, hv.w)};
+            const uint4 h = hv[ip][it];
+            const uint4 y = {dgelu_bf2(raw.x, h.x), dgelu_bf2(raw.y, h.y), dgelu_bf2(raw.z, h.z),
+                             dgelu_bf2(raw.w, h.w)};
             *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
           }
         }
