@@ -60,6 +60,7 @@ extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void
   if (variant == 43) return epi == 0 ? launchx<kEpiNone, 256, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true>(g, st) : 5;
   if (variant == 44) return epi == 0 ? launchx<kEpiNone, 192, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 192, true>(g, st) : 5;
   if (variant == 45) return epi == 0 ? launchx<kEpiNone, 256, true, 224>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true, 224>(g, st) : 5;
+  if (variant == 55) { g_persist = 256; return launch_epi<128, 64, 2, 224>(g, epi, st); }
   if (variant == 53) { g_persist = 256; return launch_epi<192, 64, 2, 224>(g, epi, st); }
   if (variant == 50) { g_persist = 256; return launch_epi<256, 32, 3, 224>(g, epi, st); }
   if (variant == 51) { g_persist = 256; return launch_epi<192, 64, 2, 192>(g, epi, st); }

@@ -24,7 +24,7 @@ NAMES = {0: "256x256 bk32 ns3", 1: "256x192 bk32 ns3", 2: "256x192 bk32 ns4", 3:
 # 192 x 192 bk64 ns2, 224 x 192 bk64 ns2 (tile heights that fill 256 CUs at M = 25,216 / 18,464)
 
 
-def bench(fn, iters=20):
+def bench(fn, iters=40):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -59,7 +59,8 @@ def main():
         ("s_qkv", Ms, 384, 1152, 0), ("s_oproj", Ms, 384, 384, 0), ("s_ff1", Ms, 384, 1536, 1),
         ("s_ff2", Ms, 1536, 384, 0), ("s_ff1dx", Ms, 384, 1536, 2), ("s_qkvdx", Ms, 1152, 384, 0),
         ("b_qkv", Mb, 768, 2304, 0), ("b_ff1", Mb, 768, 3072, 1), ("b_ff2", Mb, 3072, 768, 0),
-        ("b_qkvdx", Mb, 2304, 768, 0), ("b_oproj", Mb, 768, 768, 0), ("big", 4096, 4096, 4096, 0),
+        ("b_qkvdx", Mb, 2304, 768, 0), ("b_oproj", Mb, 768, 768, 0), ("b_ff1dx", Mb, 768, 3072, 2),
+        ("big", 4096, 4096, 4096, 0),
     ]
     if "shapes" in args:
         shapes = [s for s in shapes if s[0] in args["shapes"].split(",")]
