@@ -530,15 +530,15 @@ static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hip
 }
 
 // the LDS-DMA form of the plain weight-gradient kernel (gemm_dw8.h)
-template <int NG>
+template <int NG, int NS = kDw8NS>
 static int dw8_launch(const DwArgs& a, bool bias, long long grid, hipStream_t st) {
-  constexpr int lds = dw8_lds_bytes<NG>();
-  const void* fn = bias ? (const void*)gemm_dw8_kernel<true, NG> : (const void*)gemm_dw8_kernel<false, NG>;
+  constexpr int lds = dw8_lds_bytes<NG, NS>();
+  const void* fn = bias ? (const void*)gemm_dw8_kernel<true, NG, NS> : (const void*)gemm_dw8_kernel<false, NG, NS>;
   if (int rc = lds_attr(fn, lds)) return rc;
   if (bias)
-    hipLaunchKernelGGL((gemm_dw8_kernel<true, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+    hipLaunchKernelGGL((gemm_dw8_kernel<true, NG, NS>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
   else
-    hipLaunchKernelGGL((gemm_dw8_kernel<false, NG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+    hipLaunchKernelGGL((gemm_dw8_kernel<false, NG, NS>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
   return 0;
 }
 
@@ -1106,8 +1106,13 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
   // partial traffic (output projection dW + reduce 34.8 -> 30.6 us); one for the larger ViT-B
   // outputs, where halving the splits would leave CUs idle (FF 139 -> 205 us)
   const int tiles = ((I + kDwT - 1) / kDwT) * ((J + kDwT - 1) / kDwT);
-  const int NG = tiles <= 64 ? 2 : 1;
-  dw_plan(M, I, J, &a.S, &a.chunk, 512 / NG);
+  int NG = tiles <= 64 ? 2 : 1;
+  int dw8v = 0;   // dev A/B: 1 = one 4-wave group with an 8-deep ring (one workgroup per CU)
+#ifdef SAE_DEV_KNOBS
+  dw8v = dev_knob("SAE_DW8_VARIANT");
+  if (dw8v == 1) NG = 1;
+#endif
+  dw_plan(M, I, J, &a.S, &a.chunk, dw8v == 1 ? 256 : 512 / NG);
   if ((long long)(a.chunk + 4 * NG * kDwK) * std::max(ldx, ldy) * 2 >= (1LL << 31))
     return fail(SAE_EUNSUPPORTED, "gemm_dw: token chunk exceeds 32-bit buffer addressing");
   a.part = reinterpret_cast<float*>(workspace);
@@ -1129,7 +1134,9 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
 #ifdef SAE_DEV_KNOBS
   dma = !dev_knob("SAE_DW_OLD");
 #endif
-  if (dma) {
+  if (dma && dw8v == 1) {
+    if (int rc = dw8_launch<1, 8>(a, db != nullptr, grid, st)) return rc;
+  } else if (dma) {
     if (int rc = NG == 2 ? dw8_launch<2>(a, db != nullptr, grid, st) : dw8_launch<1>(a, db != nullptr, grid, st))
       return rc;
   } else if (NG == 2) {

@@ -25,14 +25,27 @@ constexpr int kDw8K = 32;                  // tokens per stage
 constexpr int kDw8NS = 4;                  // ring depth per wave group
 constexpr int kDw8Img = kDw8K * 256;       // one [32][128] bf16 operand image (8 KiB)
 constexpr int kDw8Stage = 2 * kDw8Img;     // X + dY
-template <int NG> constexpr int dw8_lds_bytes() {
-  constexpr int ring = NG * kDw8NS * kDw8Stage;
+template <int NG, int NS = kDw8NS> constexpr int dw8_lds_bytes() {
+  constexpr int ring = NG * NS * kDw8Stage;
   constexpr int red = NG == 2 ? 4 * 16384 + 4 * 8192 : 0;   // group 1 -> group 0 hand-off
   return ring > red ? ring : red;
 }
 
-template <bool BIAS, int NG>
-__global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void gemm_dw8_kernel(DwArgs a) {
+// counted wait for the oldest stage with `ahead` younger stages (4 DMA instructions each) in flight
+template <int N> __device__ __forceinline__ void dw8_wait(int ahead) {
+  if constexpr (N > 0) {
+    if (ahead >= N) {
+      g8_wait_barrier<4 * N>();
+      return;
+    }
+    dw8_wait<N - 1>(ahead);
+  } else {
+    g8_wait_barrier<0>();
+  }
+}
+
+template <bool BIAS, int NG, int NS = kDw8NS>
+__global__ __launch_bounds__(256 * NG, NG == 1 && NS <= 4 ? 2 : 1) void gemm_dw8_kernel(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_all[];
   const int ti = (a.I + kDwT - 1) / kDwT, tj = (a.J + kDwT - 1) / kDwT;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);   // as gemm_dw_kernel: a chunk's tiles on one XCD
@@ -48,8 +61,8 @@ __global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void gemm_dw8_kernel(DwA
   const bool bias = BIAS && it == 0 && wi == 0;
   const unsigned lring = __builtin_amdgcn_readfirstlane(
       (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem_all)) +
-      (unsigned)(grp * kDw8NS * kDw8Stage);
-  const char* ring = smem_all + grp * kDw8NS * kDw8Stage;
+      (unsigned)(grp * NS * kDw8Stage);
+  const char* ring = smem_all + grp * NS * kDw8Stage;
 
   const g8_u32x4 rx = g8_rsrc(a.x + (long long)m0 * a.ldx, m1 - m0, a.ldx);
   const g8_u32x4 ry = g8_rsrc(a.dy + (long long)m0 * a.ldy, m1 - m0, a.ldy);
@@ -69,7 +82,7 @@ __global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void gemm_dw8_kernel(DwA
   const int nst = ((m1 - m0 + kDw8K - 1) / kDw8K + NG - 1) / NG;
   auto issue = [&](int q) __attribute__((always_inline)) {
     const int st = q * NG + grp;
-    const unsigned lb = lring + (unsigned)((q % kDw8NS) * kDw8Stage);
+    const unsigned lb = lring + (unsigned)((q % NS) * kDw8Stage);
     g8_dma2(rx, vx[0] + (unsigned)st * stx, vx[1] + (unsigned)st * stx, lb + 1024u * w, lb + 1024u * (w + 4));
     g8_dma2(ry, vy[0] + (unsigned)st * sty, vy[1] + (unsigned)st * sty, lb + kDw8Img + 1024u * w,
             lb + kDw8Img + 1024u * (w + 4));
@@ -103,16 +116,13 @@ __global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void gemm_dw8_kernel(DwA
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
 #pragma unroll
-  for (int q = 0; q < kDw8NS - 1; ++q)
+  for (int q = 0; q < NS - 1; ++q)
     if (q < nst) issue(q);
   for (int g = 0; g < nst; ++g) {
-    const int ahead = min(kDw8NS - 2, nst - 1 - g);   // younger stages in flight
-    if (ahead >= 2) g8_wait_barrier<8>();
-    else if (ahead == 1) g8_wait_barrier<4>();
-    else g8_wait_barrier<0>();
+    dw8_wait<NS - 2>(min(NS - 2, nst - 1 - g));   // younger stages still in flight
     __builtin_amdgcn_sched_barrier(0);
-    if (g + kDw8NS - 1 < nst) issue(g + kDw8NS - 1);
-    const char* imx = ring + (g % kDw8NS) * kDw8Stage;
+    if (g + NS - 1 < nst) issue(g + NS - 1);
+    const char* imx = ring + (g % NS) * kDw8Stage;
     const char* imy = imx + kDw8Img;
 #pragma unroll
     for (int k = 0; k < kDw8K / 16; ++k) {
