@@ -203,6 +203,15 @@ int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t j
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
                 const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
                 int32_t epilogue, const void* aux, int64_t ldaux, void* c2);
+/* Same, with a workspace of sae_gemm_nt_workspace_bytes(M, N, K, epilogue) bytes (16-byte
+   aligned; NULL or 0 bytes: none used).  Deep, narrow shapes whose tiles leave compute units idle
+   (the 768-feature outputs at K >= 2,048) then run stream-K: the K loop of all tiles split evenly
+   over one workgroup per CU, split tiles summed in a fixed order through the workspace
+   (deterministic).  The workspace is used by one call at a time (stream-ordered). */
+size_t sae_gemm_nt_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t epilogue);
+int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
+                   const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
+                   int32_t epilogue, const void* aux, int64_t ldaux, void* c2, void* workspace);
 /* The same projections at compute dtype float32 (the reference's fp32 trunks, cait.py:147-154,
    and every fp32 run), on the exact-f32 MFMA:
      c[m][n] = (accumulate ? c[m][n] : 0) + sum_k A(m,k) B(k,n) (+ bias[n])

@@ -615,6 +615,33 @@ static bool g8x_route(int M, int N, int K, int epilogue) {
   return epilogue != SAE_EPI_DGELU && N == 768 && K >= 768 && K % 64 == 0 && M >= 4096;
 }
 
+// stream-K form (gemm8s) for the deep 768-feature outputs: one workgroup per CU, a fixed-order
+// fix-up of the tiles split between workgroups through `workspace` (gemm8.h)
+static constexpr bool kG8sOn = false;   // stream-K routing (measured in tools/probe first)
+static bool g8s_route(int M, int N, int K, int epilogue) {
+  bool on = kG8sOn;
+#ifdef SAE_DEV_KNOBS
+  on = on || dev_knob("SAE_NT_SK");
+#endif
+  if (!on) return false;
+  const int G = device_cus();
+  if (epilogue != SAE_EPI_NONE || N != 768 || K < 2048 || K % 32 || M < 4096 || G % 8 || G > 1024) return false;
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  // fewer tiles than CUs (else plain gemm8x), >= 2 K-tiles per workgroup in every XCD, 32-bit ranges
+  return tiles < G && (tiles / 8) * (K / 32) >= 2 * (G / 8) && tiles * (K / 32) < (1LL << 24);
+}
+static size_t g8s_workspace_bytes() { return (size_t)device_cus() * (256 * 256 * 4 + 4) + 256; }
+static int g8s_launch(NtArgs g, hipStream_t st, void* workspace) {
+  const int G = device_cus();
+  g.skpart = reinterpret_cast<float*>(workspace);
+  g.skflag = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + (size_t)G * 256 * 256 * 4);
+  if (hipMemsetAsync(g.skflag, 0, (size_t)G * 4, st) != hipSuccess) return fail(SAE_EHIP, "gemm8s: flag reset failed");
+  constexpr int lds = g8x_lds_bytes<256>();
+  if (int rc = lds_attr((const void*)gemm8s_nt_kernel<256>, lds)) return rc;
+  hipLaunchKernelGGL((gemm8s_nt_kernel<256>), dim3((unsigned)G), dim3(512), lds, st, g);
+  return check_launch("gemm8s_nt");
+}
+
 // gemm8 (gemm8.h) or the 128-row sae_gemm_nt: tools/probe/gemm8_probe.py, profiles/r04c_g8probe.txt --
 // gemm8 wins on the 384-feature outputs at every depth (DeiT-S / CaiT output projection, QKV and
 // FF Dense_0 input gradients, Dense_1 forward: 412-692 -> 497-849 TF/s) and on the wide K = 768
@@ -1230,9 +1257,20 @@ int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, 
 }
 
 // ------------------------------------------------------------ forward / input-gradient GEMMs
+size_t sae_gemm_nt_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
+  if (M < 1 || N < 1 || K < 1) return 0;
+  return g8s_route(M, N, K, epilogue) ? g8s_workspace_bytes() : 0;
+}
+
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
                 int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
                 int64_t ldaux, void* c2) {
+  return sae_gemm_nt_ws(stream, M, N, K, a, lda, bt, ldb, bias, c, ldc, epilogue, aux, ldaux, c2, nullptr);
+}
+
+int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
+                   int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
+                   int64_t ldaux, void* c2, void* workspace) {
   if (M < 1 || N < 1 || K < 1) return fail(SAE_EINVAL, "gemm_nt: M/N/K must be >= 1 (got %d/%d/%d)", M, N, K);
   if (K % kNtK || N % 8)
     return fail(SAE_EUNSUPPORTED, "gemm_nt: K (%d) must be a multiple of %d and N (%d) of 8", K, kNtK, N);
@@ -1265,6 +1303,14 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   g.ldc = ldc;
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
+  if (workspace && g8s_route(M, N, K, epilogue)
+#ifdef SAE_DEV_KNOBS
+      && !dev_knob("SAE_NT_NO_G8") && !dev_knob("SAE_NT_NO_SK")
+#endif
+  ) {
+    if (!aligned16(workspace)) return fail(SAE_EINVAL, "gemm_nt: workspace must be 16-byte aligned");
+    return g8s_launch(g, st, workspace);
+  }
   if (g8x_route(M, N, K, epilogue)
 #ifdef SAE_DEV_KNOBS
       && !dev_knob("SAE_NT_NO_G8")

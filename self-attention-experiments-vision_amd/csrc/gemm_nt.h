@@ -39,6 +39,8 @@ struct NtArgs {
   int M, N, K;
   long long lda, ldb, ldc, ldaux;
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
+  float* skpart;       // stream-K (gemm8.h gemm8s): fp32 partial tile per workgroup
+  int* skflag;         // stream-K: one flag per workgroup (zero at launch; reset by the reader)
 };
 
 constexpr int kNtT = 128;   // output tile edge

@@ -1082,8 +1082,12 @@ def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = N
         aux = aux.contiguous()
     if bias is not None:
         bias = bias.float().contiguous()
-    L.check(lib.sae_gemm_nt(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias), _ptr(c),
-                            c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0, _ptr(c2)))
+    # stream-K shapes (the deep 768-feature outputs) take a workspace for their split tiles
+    nbytes = lib.sae_gemm_nt_workspace_bytes(M, N, K, int(epilogue))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=a2.device) if nbytes else None
+    L.check(lib.sae_gemm_nt_ws(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias),
+                               _ptr(c), c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0,
+                               _ptr(c2), _ptr(ws)))
     return (c, c2) if epilogue == EPI_GELU else c
 
 

@@ -35,6 +35,27 @@ static int launchx(const NtArgs& g, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+// stream-K ping-pong (gemm8s): one workgroup per CU, workspace kept across calls, flags zeroed
+// before each launch
+static float* g_skpart = nullptr;
+static int* g_skflag = nullptr;
+static int launchs(NtArgs g, hipStream_t st) {
+  constexpr int lds = g8x_lds_bytes<256>();
+  const void* fn = (const void*)gemm8s_nt_kernel<256>;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return 2;
+  if (g.K % 32) return 4;
+  const int G = 256;
+  if (!g_skpart) {
+    if (hipMalloc(&g_skpart, (size_t)G * 256 * 256 * 4) != hipSuccess) return 6;
+    if (hipMalloc(&g_skflag, (size_t)G * 4) != hipSuccess) return 6;
+  }
+  if (hipMemsetAsync(g_skflag, 0, (size_t)G * 4, st) != hipSuccess) return 7;
+  g.skpart = g_skpart;
+  g.skflag = g_skflag;
+  hipLaunchKernelGGL((gemm8s_nt_kernel<256>), dim3(G), dim3(512), lds, st, g);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void* a, long long lda, const void* bt,
                       long long ldb, const float* bias, void* c, long long ldc, int epi, const void* aux,
                       long long ldaux, void* c2) {
@@ -59,6 +80,7 @@ extern "C" int g8_run(int variant, void* stream, int M, int N, int K, const void
   if (variant == 41) return epi == 0 ? launchx<kEpiNone, 192>(g, st) : epi == 1 ? launchx<kEpiGelu, 192>(g, st) : 5;
   if (variant == 43) return epi == 0 ? launchx<kEpiNone, 256, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true>(g, st) : 5;
   if (variant == 44) return epi == 0 ? launchx<kEpiNone, 192, true>(g, st) : epi == 1 ? launchx<kEpiGelu, 192, true>(g, st) : 5;
+  if (variant == 46) return epi == 0 ? launchs(g, st) : 5;
   if (variant == 45) return epi == 0 ? launchx<kEpiNone, 256, true, 224>(g, st) : epi == 1 ? launchx<kEpiGelu, 256, true, 224>(g, st) : 5;
   if (variant == 55) { g_persist = 256; return launch_epi<128, 64, 2, 224>(g, epi, st); }
   if (variant == 53) { g_persist = 256; return launch_epi<192, 64, 2, 224>(g, epi, st); }
