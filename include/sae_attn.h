@@ -194,7 +194,7 @@ int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t j
      SAE_EPI_NONE : c = bf16(acc + bias)
      SAE_EPI_GELU : c2 = h = bf16(acc + bias), c = bf16(gelu(h))
      SAE_EPI_DGELU: c = bf16(bf16(acc) * gelu'(aux))   (aux bf16 [M][N], ldaux; bias NULL)
-   c, c2 bf16 [M][N] (ldc); bias fp32 [N] or NULL.  K a multiple of 64; N, lda, ldb, ldc
+   c, c2 bf16 [M][N] (ldc); bias fp32 [N] or NULL.  K a multiple of 8; N, lda, ldb, ldc
    multiples of 8; pointers 16-byte aligned.  A Dense forward passes the transposed bf16
    kernel as bt (see sae_weight_cast); its input gradient passes the kernel itself. */
 #define SAE_EPI_NONE 0
@@ -203,15 +203,14 @@ int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t j
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
                 const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
                 int32_t epilogue, const void* aux, int64_t ldaux, void* c2);
-/* Same, with a workspace of sae_gemm_nt_workspace_bytes(M, N, K, epilogue) bytes (16-byte
-   aligned; NULL or 0 bytes: none used).  Deep, narrow shapes whose tiles leave compute units idle
-   (the 768-feature outputs at K >= 2,048) then run stream-K: the K loop of all tiles split evenly
-   over one workgroup per CU, split tiles summed in a fixed order through the workspace
-   (deterministic).  The workspace is used by one call at a time (stream-ordered). */
-size_t sae_gemm_nt_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t epilogue);
-int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
-                   const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
-                   int32_t epilogue, const void* aux, int64_t ldaux, void* c2, void* workspace);
+/* Which kernel sae_gemm_nt runs for a shape (host-only, no device needed): the round-5 routing
+   rule by tile fill and reduction depth (capi.hip, g8x_route / g8_route). */
+#define SAE_NT_ROUTE_NONE 0           /* shape not supported: sae_gemm_nt returns SAE_EUNSUPPORTED */
+#define SAE_NT_ROUTE_TILE128 1        /* 128-row tiles (gemm_nt_kernel), K % 64 == 0 */
+#define SAE_NT_ROUTE_TILE128_KTAIL 2  /* 128-row tiles, K % 8 == 0 with a partial last K stage */
+#define SAE_NT_ROUTE_GEMM8 3          /* persistent 224/256 x 192 tiles, LDS-DMA (gemm8_nt_kernel) */
+#define SAE_NT_ROUTE_GEMM8X 4         /* ping-pong 256 x 256 tiles, LDS-DMA (gemm8x_nt_kernel) */
+int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue);
 /* The same projections at compute dtype float32 (the reference's fp32 trunks, cait.py:147-154,
    and every fp32 run), on the exact-f32 MFMA:
      c[m][n] = (accumulate ? c[m][n] : 0) + sum_k A(m,k) B(k,n) (+ bias[n])

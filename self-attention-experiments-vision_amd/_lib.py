@@ -71,9 +71,8 @@ _PROTOS = [
     ("sae_gemm_dw_blocked", _i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
     ("sae_gemm_f32_workspace_bytes", _sz, [_i32, _i32, _i32]),
     ("sae_gemm_f32", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _i32, _vp]),
-    ("sae_gemm_nt_workspace_bytes", _sz, [_i32, _i32, _i32, _i32]),
-    ("sae_gemm_nt_ws", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("sae_gemm_nt", _i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    ("sae_gemm_nt_route", _i32, [_i32, _i32, _i32, _i32]),
     ("sae_patch_embed_fwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp]),
     ("sae_patch_embed_bwd_workspace_bytes", _sz, [ctypes.POINTER(SaePatchDesc)]),
     ("sae_patch_embed_bwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp, _i32, _vp]),

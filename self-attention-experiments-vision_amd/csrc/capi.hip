@@ -607,39 +607,22 @@ static int g8x_launch(const NtArgs& g, hipStream_t st) {
   return g8_pick_bm(g.M, g.N, BN) == 224 ? g8x_launch_bm<EPI, BN, 224>(g, st) : g8x_launch_bm<EPI, BN, 256>(g, st);
 }
 
-// the 768-feature outputs at reduction depth >= 768 (ViT-B output projection, QKV input gradient,
-// FF Dense_1 forward, Dense_0 input gradient): the ping-pong 256 x 256 kernel, 0.90-0.98 of the
-// library there (profiles/r04i_g8probe.txt: 1,086-1,132 vs 1,180-1,265 TF/s at K 2,304 / 3,072,
-// 820 vs 833 at K 768), so that no library GEMM runs in the ViT-B step
+// Kernel choice for sae_gemm_nt (round 5: a rule on tile fill and reduction depth instead of the
+// BASELINE shape whitelist; every width in create_model.py:6-215 routes to one of these):
+//   gemm8x  (ping-pong 256 x 256 tiles): reductions K >= 768 into outputs that fill 256-wide tiles
+//           but not 192-wide ones (N % 256 == 0 and N % 192 != 0: ViT-L 1024 / 4096, CvT-W24 1024),
+//           plus the 768-feature outputs (ViT-B / CaiT-M output projection, QKV / Dense_0 input
+//           gradients, Dense_1 forward; 0.90-0.98 of the library, profiles/r04i_g8probe.txt);
+//   gemm8   (persistent 224/256 x 192 tiles): outputs that fill 192-wide tiles (N % 192 == 0) at
+//           K >= 384 -- every DeiT-S / CaiT-S projection, the ViT-B wide K = 768 forwards;
+//   128-row sae_gemm_nt: the rest -- small M (classifier heads, CLS rows), K < 384 (DeiT-Ti, the
+//           C = 192 widths), K not a multiple of 64 (KT instances: CaiT-XXS / XS 288, CvT 368, TNT
+//           inner 24 / 40 and their FF widths), the GELU' epilogue beyond K = 384 (its 256-token
+//           tile), N not a multiple of 192 or 256.
+// Both persistent kernels need M >= 4096 (enough tiles to fill the CUs) and K % 64 == 0.
 static bool g8x_route(int M, int N, int K, int epilogue) {
-  return epilogue != SAE_EPI_DGELU && N == 768 && K >= 768 && K % 64 == 0 && M >= 4096;
-}
-
-// stream-K form (gemm8s) for the deep 768-feature outputs: one workgroup per CU, a fixed-order
-// fix-up of the tiles split between workgroups through `workspace` (gemm8.h)
-static constexpr bool kG8sOn = false;   // stream-K routing (measured in tools/probe first)
-static bool g8s_route(int M, int N, int K, int epilogue) {
-  bool on = kG8sOn;
-#ifdef SAE_DEV_KNOBS
-  on = on || dev_knob("SAE_NT_SK");
-#endif
-  if (!on) return false;
-  const int G = device_cus();
-  if (epilogue != SAE_EPI_NONE || N != 768 || K < 2048 || K % 32 || M < 4096 || G % 8 || G > 1024) return false;
-  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256);
-  // fewer tiles than CUs (else plain gemm8x), >= 2 K-tiles per workgroup in every XCD, 32-bit ranges
-  return tiles < G && (tiles / 8) * (K / 32) >= 2 * (G / 8) && tiles * (K / 32) < (1LL << 24);
-}
-static size_t g8s_workspace_bytes() { return (size_t)device_cus() * (256 * 256 * 4 + 4) + 256; }
-static int g8s_launch(NtArgs g, hipStream_t st, void* workspace) {
-  const int G = device_cus();
-  g.skpart = reinterpret_cast<float*>(workspace);
-  g.skflag = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + (size_t)G * 256 * 256 * 4);
-  if (hipMemsetAsync(g.skflag, 0, (size_t)G * 4, st) != hipSuccess) return fail(SAE_EHIP, "gemm8s: flag reset failed");
-  constexpr int lds = g8x_lds_bytes<256>();
-  if (int rc = lds_attr((const void*)gemm8s_nt_kernel<256>, lds)) return rc;
-  hipLaunchKernelGGL((gemm8s_nt_kernel<256>), dim3((unsigned)G), dim3(512), lds, st, g);
-  return check_launch("gemm8s_nt");
+  if (epilogue == SAE_EPI_DGELU || K < 768 || K % 64 || M < 4096 || N % 256) return false;
+  return N == 768 || N % 192 != 0;
 }
 
 // gemm8 (gemm8.h) or the 128-row sae_gemm_nt: tools/probe/gemm8_probe.py, profiles/r04c_g8probe.txt --
@@ -652,9 +635,8 @@ static int g8s_launch(NtArgs g, hipStream_t st, void* workspace) {
 // 593 -> 647 TF/s, FF Dense_0 + GELU 546 -> 563, Dense_1 input gradient with GELU' 497 -> 509
 // (profiles/r04k_g8probe.txt, v53 vs rel)
 static bool g8_route(int M, int N, int K, int epilogue) {
-  if (N % 192 || K % 64 || K < 384 || M < 4096 || N > 3072) return false;
-  if (epilogue == SAE_EPI_DGELU) return K == 384;
-  return N == 384 || K == 384 || (K >= 768 && N >= 1152);
+  if (N % 192 || K % 64 || K < 384 || M < 4096) return false;
+  return epilogue != SAE_EPI_DGELU || K == 384;
 }
 
 extern "C" {
@@ -1257,23 +1239,19 @@ int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, 
 }
 
 // ------------------------------------------------------------ forward / input-gradient GEMMs
-size_t sae_gemm_nt_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
-  if (M < 1 || N < 1 || K < 1) return 0;
-  return g8s_route(M, N, K, epilogue) ? g8s_workspace_bytes() : 0;
+int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
+  if (M < 1 || N < 1 || K < 1 || K % 8 || N % 8 || epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_DGELU)
+    return SAE_NT_ROUTE_NONE;
+  if (g8x_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8X;
+  if (g8_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8;
+  return K % kNtK ? SAE_NT_ROUTE_TILE128_KTAIL : SAE_NT_ROUTE_TILE128;
 }
 
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
                 int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
                 int64_t ldaux, void* c2) {
-  return sae_gemm_nt_ws(stream, M, N, K, a, lda, bt, ldb, bias, c, ldc, epilogue, aux, ldaux, c2, nullptr);
-}
-
-int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda, const void* bt,
-                   int64_t ldb, const float* bias, void* c, int64_t ldc, int32_t epilogue, const void* aux,
-                   int64_t ldaux, void* c2, void* workspace) {
   if (M < 1 || N < 1 || K < 1) return fail(SAE_EINVAL, "gemm_nt: M/N/K must be >= 1 (got %d/%d/%d)", M, N, K);
-  if (K % kNtK || N % 8)
-    return fail(SAE_EUNSUPPORTED, "gemm_nt: K (%d) must be a multiple of %d and N (%d) of 8", K, kNtK, N);
+  if (K % 8 || N % 8) return fail(SAE_EUNSUPPORTED, "gemm_nt: K (%d) and N (%d) must be multiples of 8", K, N);
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8)
     return fail(SAE_EINVAL, "gemm_nt: bad leading dimensions lda %lld ldb %lld ldc %lld", (long long)lda,
                 (long long)ldb, (long long)ldc);
@@ -1303,14 +1281,6 @@ int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a,
   g.ldc = ldc;
   g.ldaux = ldaux;
   hipStream_t st = (hipStream_t)stream;
-  if (workspace && g8s_route(M, N, K, epilogue)
-#ifdef SAE_DEV_KNOBS
-      && !dev_knob("SAE_NT_NO_G8") && !dev_knob("SAE_NT_NO_SK")
-#endif
-  ) {
-    if (!aligned16(workspace)) return fail(SAE_EINVAL, "gemm_nt: workspace must be 16-byte aligned");
-    return g8s_launch(g, st, workspace);
-  }
   if (g8x_route(M, N, K, epilogue)
 #ifdef SAE_DEV_KNOBS
       && !dev_knob("SAE_NT_NO_G8")
@@ -1337,7 +1307,6 @@ int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a,
   // still gives >= 2 tiles per CU; 128 otherwise (plain GEMMs: no gain, profiles/r03n_nt_probe.txt)
   const long long tn = (N + kNtT - 1) / kNtT;
   const long long grid128 = (long long)((M + kNtT - 1) / kNtT) * tn;
-  (void)grid128;
   bool tall = epilogue != SAE_EPI_NONE && K >= 768 && (long long)((M + 255) / 256) * tn >= 512;
 #ifdef SAE_DEV_KNOBS
   const int ntv = dev_knob("SAE_NT_VARIANT");
@@ -1364,6 +1333,13 @@ int sae_gemm_nt_ws(void* stream, int32_t M, int32_t N, int32_t K, const void* a,
   // overlaps other tiles' MFMAs; same-box step A/B 9.19 -> 9.10 ms); deeper reductions (ViT-B,
   // K 768) and the plain GEMM keep 64-deep stages (2 workgroups per CU), which are faster there
   const bool shallow = K <= 384;
+  if (K % kNtK) {   // K-tail instances (K % 8 == 0): 64-deep stages, the last one partial
+    int rc = epilogue == SAE_EPI_NONE   ? nt_launch<kEpiNone, NtRowAT<64, 128, true>>(g, grid128, st)
+             : epilogue == SAE_EPI_GELU ? nt_launch<kEpiGelu, NtRowAT<64, 128, true>>(g, grid128, st)
+                                        : nt_launch<kEpiDGelu, NtRowAT<64, 128, true>>(g, grid128, st);
+    if (rc) return rc;
+    return check_launch("gemm_nt");
+  }
   if (tall) {
     const int rc = epilogue == SAE_EPI_NONE ? nt_launch<kEpiNone, NtRowAT<32, 256>>(g, grid, st)
                    : epilogue == SAE_EPI_GELU ? nt_launch<kEpiGelu, NtRowAT<32, 256>>(g, grid, st)

@@ -485,246 +485,6 @@ __global__ __launch_bounds__(512, 1) void gemm8x_nt_kernel(NtArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Stream-K form of the ping-pong kernel, for the deep 768-feature outputs (ViT-B Dense_1 forward,
-// QKV and Dense_0 input gradients at K = 2,304 / 3,072): their 219 tiles of 256 x 256 leave 37 of
-// 256 CUs idle in gemm8x_nt_kernel.  Here the grid is one workgroup per CU and the K-tiles of all
-// output tiles form one iteration space, cut into equal contiguous ranges:
-//   * the tiles are first divided among the 8 XCDs (whole tiles, in order), and an XCD's
-//     iteration range among its workgroups (blockIdx = 8 slot + xcd: round-robin dispatch puts
-//     workgroup b on XCD b % 8), so every partial tile moves through one L2;
-//   * a workgroup walks its range in order; a segment of a tile that does not start at K = 0 is a
-//     PRODUCER segment (its first in time): its fp32 accumulators go to the workgroup's slot of
-//     `skpart` (waited into the XCD's L2) and its flag is raised;
-//   * the segment that starts at K = 0 but ends early is the tile's FINISHER (the workgroup's last
-//     segment): it waits for the flags of the higher slots covering the rest of the tile, adds their
-//     partials (read from the shared L2, past its L1) in slot order -- fixed order: deterministic --
-//     and runs the epilogue.  Producer and finisher share an XCD by construction, so neither
-//     needs an agent-scope fence (an L2 write-back / invalidate per split tile halved throughput);
-//   * a finisher waits only on producer segments, which are the FIRST thing their workgroups do,
-//     and only on higher slots of its own XCD: once a workgroup is dispatched it produces before it
-//     waits, so the wait needs no more than that every workgroup is eventually dispatched (other
-//     kernels on other streams can delay, not block it).  The spin is bounded (a flag that never
-//     comes lets the grid drain with a wrong tile rather than hang).
-// EPI none only (the routed shapes have no epilogue); BM = 256, BN = 256.
-template <int BN>
-__global__ __launch_bounds__(512, 1) void gemm8s_nt_kernel(NtArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BM = 256;
-  using C = G8Cfg<BN, BM>;
-  static_assert(C::MT == 8, "256-row tiles");
-  constexpr int RB = 64;
-  constexpr int IMGA = 256 * RB, STAGE = (256 + BN) * RB;
-  constexpr int PBT = BN / 16;
-  constexpr int PB0 = (PBT + 7) / 8, PB1 = PBT / 8, PBX = PBT % 8;
-  constexpr int TILEF = BM * BN;                 // floats per partial tile
-
-  const int tn = (a.N + BN - 1) / BN;
-  const int ntile = ((a.M + BM - 1) / BM) * tn;
-  const int nkt = a.K / 32;
-  const int G = gridDim.x, SPX = G / 8;          // G a multiple of 8 (host)
-  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-  // (all in 32 bits: the host routes only tiles * K-tiles < 2^24 here)
-  const int t0 = ntile * xcd / 8, t1 = ntile * (xcd + 1) / 8;
-  const int nx = (t1 - t0) * nkt;                // this XCD's iterations
-  auto range_start = [&](int sl) __attribute__((always_inline)) -> int {
-    return __builtin_amdgcn_readfirstlane(t0 * nkt + nx * sl / SPX);
-  };
-  const int it0 = range_start(slot), it1 = range_start(slot + 1);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = w >> 2, wc = w & 3;
-  const unsigned lbase = __builtin_amdgcn_readfirstlane(
-      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
-  const int prow = lane >> 2, pc = lane & 3;
-  unsigned goa[2], gob[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * (w + 8 * i) + prow;
-    goa[i] = (unsigned)(((long long)row * a.lda + 8 * (pc ^ g8_swz<32>(row))) * 2);
-    gob[i] = (unsigned)(((long long)row * a.ldb + 8 * (pc ^ g8_swz<32>(row))) * 2);
-  }
-  const bool bx = PBX == 0 || w < PBX;
-  g8_u32x4 ra, rb;
-  auto issue_a = [&](int kt) __attribute__((always_inline)) {
-    const unsigned ko = (unsigned)kt * RB;
-    const unsigned lb = lbase + (unsigned)((kt & 3) * STAGE);
-    g8_dma2(ra, goa[0] + ko, goa[1] + ko, lb + 1024u * w, lb + 1024u * (w + 8));
-  };
-  auto issue_b = [&](int kt) __attribute__((always_inline)) {
-    const unsigned ko = (unsigned)kt * RB;
-    const unsigned lb = lbase + (unsigned)((kt & 3) * STAGE);
-    if (PB0 == 2 && bx)
-      g8_dma2(rb, gob[0] + ko, gob[1] + ko, lb + IMGA + 1024u * w, lb + IMGA + 1024u * (w + 8));
-    else if (PB0 >= 1 && (PB1 >= 1 || bx))
-      g8_dma1(rb, gob[0] + ko, lb + IMGA + 1024u * w);
-  };
-  const int fr = lane & 15, fg = lane >> 4;
-  const int co = 16 * (fg ^ g8_swz<32>(fr));
-  const char* pa0 = smem + (C::WM * grp + fr) * RB + co;
-  const char* pb0 = smem + IMGA + (C::WN * wc + fr) * RB + co;
-  f32x4 acc[C::MT][C::NT];
-
-  // the ping-pong K loop of gemm8x_nt_kernel (BAL) over K-tiles [ka, kb) of the current tile
-  auto run = [&](int ka, int kb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    issue_a(ka);
-    issue_b(ka);
-    if (ka + 1 < kb) {
-      issue_a(ka + 1);
-      issue_b(ka + 1);
-      if (bx) g8_wait_barrier<2 + PB0>(); else g8_wait_barrier<2 + PB1>();
-    } else {
-      g8_wait_barrier<0>();
-    }
-    if (grp == 1) asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    for (int kt = ka; kt < kb; ++kt) {
-      const char* ia = pa0 + (kt & 3) * STAGE;
-      const char* ib = pb0 + (kt & 3) * STAGE;
-      bf16x8 bf[C::NT], af[4];
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(ib + 16 * j * RB);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * i * RB);
-      if (kt + 2 < kb) issue_a(kt + 2);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ia + 16 * (4 + i) * RB);
-      if (kt + 1 < kb) {
-        if (kt + 2 < kb) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (kt + 2 < kb) issue_b(kt + 2);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (grp == 0) asm volatile("s_barrier" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");   // every wave done with the ring
-  };
-  // partial tile of slot sl through a buffer descriptor: wave w's (i, j) accumulator is 1 KiB at
-  // byte (w MT NT + i NT + j) KiB + 16 lane -- the (i, j) part rides in the scalar offset, so the
-  // 32 stores / loads of a tile need one address VGPR
-  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-  const int pvo = (w * C::MT * C::NT * 64 + lane) * 16;
-  auto part = [&](int sl) __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(a.skpart + (size_t)sl * TILEF, (short)0, TILEF * 4, 0x00020000);
-  };
-  auto epilogue = [&](int m0, int n0) __attribute__((always_inline)) {
-    constexpr int SRB = C::WN * 2 + 16, SCH = C::WN / 8;
-    char* scratch = smem + w * (C::WM * SRB);
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    const int nw = n0 + C::WN * wc;
-    f32x4 bv[C::NT];
-#pragma unroll
-    for (int j = 0; j < C::NT; ++j) {
-      const int n = nw + 16 * j + 4 * fg;
-      bv[j] = (a.bias && n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j) {
-        const bf16x4 v = {(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
-                          (__bf16)(acc[i][j][2] + bv[j][2]), (__bf16)(acc[i][j][3] + bv[j][3])};
-        *reinterpret_cast<bf16x4*>(scratch + (16 * i + fr) * SRB + 2 * (16 * j + 4 * fg)) = v;
-      }
-    __builtin_amdgcn_wave_barrier();
-    const int mw = m0 + C::WM * grp;
-#pragma unroll 4
-    for (int it = 0; it < C::WM * SCH / 64; ++it) {
-      const int id = it * 64 + lane;
-      const int rr = id / SCH, c = id % SCH;
-      const uint4 raw = *reinterpret_cast<const uint4*>(scratch + rr * SRB + 16 * c);
-      const int m = mw + rr, n = nw + 8 * c;
-      if (m < a.M && n < a.N) *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
-    }
-    __syncthreads();   // scratch (the ring) free before the next segment's DMA
-  };
-
-  auto set_tile = [&](int t) __attribute__((always_inline)) {
-    const int m0 = (t / tn) * BM, n0 = (t % tn) * BN;
-    ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(BM, a.M - m0), a.lda);
-    rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
-  };
-  int it = it0;
-  // 1. a first segment that starts inside a tile: PRODUCER (partial to this slot, flag raised)
-  if (it < it1 && it % nkt != 0) {
-    const int t = it / nkt, ka = it - t * nkt;
-    const int kb = min(nkt, ka + (it1 - it));
-    set_tile(t);
-    run(ka, kb);
-    const __amdgpu_buffer_rsrc_t p = part(blockIdx.x);
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-      for (int j = 0; j < C::NT; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), p, pvo, (i * C::NT + j) * 1024, 0);
-    // the partial must sit in this XCD's L2 (which the finisher shares) before the flag: every
-    // wave waits for its stores; no agent-scope release (its L2 write-back cost 2x in the probe)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.skflag + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    it += kb - ka;
-  }
-  // 2. whole tiles
-  for (; it + nkt <= it1; it += nkt) {
-    const int t = it / nkt;
-    set_tile(t);
-    run(0, nkt);
-    epilogue((t / tn) * BM, (t % tn) * BN);
-  }
-  // 3. a last segment that starts a tile and ends inside it: FINISHER (adds the higher slots'
-  // partials of K-tiles [kb, nkt), in slot order, then the epilogue)
-  if (it < it1) {
-    const int t = it / nkt, kb = it1 - it;
-    set_tile(t);
-    run(0, kb);
-    const int tend = (t + 1) * nkt;
-    for (int sl = slot + 1; sl < SPX && range_start(sl) < tend; ++sl) {
-      const int b = 8 * sl + xcd;
-      if (tid == 0) {
-        int spins = 0;
-        while (__hip_atomic_load(a.skflag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1 << 22))
-          __builtin_amdgcn_s_sleep(2);
-        __hip_atomic_store(a.skflag + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      // the partial is read from the shared L2 past this CU's L1 (sc0): no agent-scope acquire,
-      // whose L2 invalidate would send every workgroup of the XCD back to HBM for its operands
-      const __amdgpu_buffer_rsrc_t p = part(b);
-#pragma unroll
-      for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j)
-          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(p, pvo, (i * C::NT + j) * 1024, 1));
-    }
-    epilogue((t / tn) * BM, (t % tn) * BN);
-  }
-}
-
 template <int BN, int BM = 256> constexpr int g8x_lds_bytes() {
   constexpr int ring = 4 * (256 + BN) * 64, scratch = 8 * (BM / 2) * (BN / 4 * 2 + 16);
   return ring > scratch ? ring : scratch;

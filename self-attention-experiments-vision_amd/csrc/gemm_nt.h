@@ -39,8 +39,6 @@ struct NtArgs {
   int M, N, K;
   long long lda, ldb, ldc, ldaux;
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
-  float* skpart;       // stream-K (gemm8.h gemm8s): fp32 partial tile per workgroup
-  int* skflag;         // stream-K: one flag per workgroup (zero at launch; reset by the reader)
 };
 
 constexpr int kNtT = 128;   // output tile edge
@@ -91,13 +89,17 @@ __device__ __forceinline__ unsigned dgelu_bf2(unsigned dw, unsigned hw) {   // d
   return f2_to_bf2(bf2_to_f2(dw) * ((x * q) * poly + s));
 }
 
-// one operand's ROWS x BK stage: ROWS * BK / 8 16-byte chunks, ROWS * BK / 2048 per thread
-template <int BK, int ROWS = 128> struct NtStageT {
+// one operand's ROWS x BK stage: ROWS * BK / 8 16-byte chunks, ROWS * BK / 2048 per thread.
+// KT (K a multiple of 8 but not of BK: the CaiT-XXS / XS 288-wide, CvT 368-wide and TNT inner
+// 24 / 40-wide projections): chunks at or past column K of the last stage read zero through the
+// descriptor's range check (offset 0x80000000), so the MFMAs add zeros there.
+template <int BK, int ROWS = 128, bool KT = false> struct NtStageT {
   static constexpr int CPR = BK / 8;         // 16-byte chunks per row
   static constexpr int PER = ROWS * CPR / 256;
   uint4 v[PER];
   unsigned goff[PER];
   unsigned loff[PER];
+  int kc[KT ? PER : 1];                      // KT: the chunk's first column inside the stage
   __device__ __forceinline__ void init(int tid, long long ld) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -105,12 +107,17 @@ template <int BK, int ROWS = 128> struct NtStageT {
       const int r = id / CPR, c = id % CPR;
       goff[i] = (unsigned)(((long long)r * ld + 8 * c) * 2);
       loff[i] = r * (BK * 2) + 16 * (c ^ swz<BK>(r));
+      if constexpr (KT) kc[i] = 8 * c;
     }
   }
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned koff) {
+  // kleft: columns of this stage that exist (K - st BK; only read with KT)
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned koff, int kleft = BK) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i] + koff, 0, 0));
+    for (int i = 0; i < PER; ++i) {
+      unsigned off = goff[i] + koff;
+      if constexpr (KT) off = kc[i] < kleft ? off : 0x80000000u;
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
   }
   __device__ __forceinline__ void write(char* img) const {
 #pragma unroll
@@ -122,15 +129,16 @@ using NtStage = NtStageT<kNtK>;
 // A-operand loader of the plain GEMM: rows m0 .. m0 + ROWS - 1 of the row-major a [M][K] through
 // a buffer descriptor (rows past M read zero).  patch.h supplies the patch-gather loaders (64-deep
 // stages, 128 rows); a loader also maps GEMM row m to its output row (orow).
-template <int BK, int ROWS = 128> struct NtRowAT {
+template <int BK, int ROWS = 128, bool KT = false> struct NtRowAT {
   static constexpr int kBK = BK;
-  NtStageT<BK, ROWS> s;
+  static constexpr bool kKT = KT;
+  NtStageT<BK, ROWS, KT> s;
   __amdgpu_buffer_rsrc_t rs;
   __device__ __forceinline__ void init(const NtArgs& a, int tid, int m0) {
     rs = row_rsrc(a.a + (long long)m0 * a.lda, min(ROWS, a.M - m0), a.lda);
     s.init(tid, a.lda);
   }
-  __device__ __forceinline__ void load(const NtArgs&, int st) { s.load(rs, (unsigned)st * (BK * 2)); }
+  __device__ __forceinline__ void load(const NtArgs& a, int st) { s.load(rs, (unsigned)st * (BK * 2), a.K - st * BK); }
   __device__ __forceinline__ void write(char* img) const { s.write(img); }
   static __device__ __forceinline__ long long orow(const NtArgs&, int m) { return m; }
 };
@@ -144,12 +152,14 @@ template <int NB> struct NtDmaA {
 };
 
 template <class AL> struct NtDepth { static constexpr int value = kNtK; };
-template <int BK, int ROWS> struct NtDepth<NtRowAT<BK, ROWS>> { static constexpr int value = BK; };
+template <int BK, int ROWS, bool KT> struct NtDepth<NtRowAT<BK, ROWS, KT>> { static constexpr int value = BK; };
 template <int NB> struct NtDepth<NtDmaA<NB>> { static constexpr int value = 32; };
 template <class AL> struct NtIsDma { static constexpr bool value = false; };
 template <int NB> struct NtIsDma<NtDmaA<NB>> { static constexpr bool value = true; };
 template <class AL> struct NtRows { static constexpr int value = kNtT; };
-template <int BK, int ROWS> struct NtRows<NtRowAT<BK, ROWS>> { static constexpr int value = ROWS; };
+template <int BK, int ROWS, bool KT> struct NtRows<NtRowAT<BK, ROWS, KT>> { static constexpr int value = ROWS; };
+template <class AL> struct NtKT { static constexpr bool value = false; };
+template <int BK, int ROWS> struct NtKT<NtRowAT<BK, ROWS, true>> { static constexpr bool value = true; };
 
 // Main loop, operands staged global -> registers -> LDS: two LDS buffers, two register sets in
 // flight.  Straight-line staging (no data-dependent branches around the loads and LDS writes):
@@ -163,18 +173,19 @@ __device__ __forceinline__ void nt_loop_regs(const NtArgs& a, int m0, int n0, in
   constexpr int IMGA = TM * BK * 2, IMG = kNtT * BK * 2, BUF = IMGA + IMG;
   // rows past N read zero through the descriptor's range check
   const __amdgpu_buffer_rsrc_t rb = row_rsrc(a.bt + (long long)n0 * a.ldb, min(kNtT, a.N - n0), a.ldb);
+  constexpr bool KT = NtKT<AL>::value;
   AL as[2];
-  NtStageT<BK> bs[2];
+  NtStageT<BK, 128, KT> bs[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     as[q].init(a, tid, m0);
     bs[q].init(tid, a.ldb);
   }
-  const int nst = a.K / BK;
+  const int nst = (a.K + BK - 1) / BK;   // KT: the last stage is partial
   as[0].load(a, 0);
-  bs[0].load(rb, 0);
+  bs[0].load(rb, 0, a.K);
   as[1].load(a, 1);
-  bs[1].load(rb, BK * 2);
+  bs[1].load(rb, BK * 2, a.K - BK);
   preload();
   as[0].write(smem);
   bs[0].write(smem + IMGA);
@@ -187,7 +198,7 @@ __device__ __forceinline__ void nt_loop_regs(const NtArgs& a, int m0, int n0, in
       char* nxt = smem + (bsel ^ 1) * BUF;
       // register set bsel went to LDS at the end of the previous stage: refill it (stage + 2)
       as[bsel].load(a, st + bsel + 2);
-      bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (BK * 2));
+      bs[bsel].load(rb, (unsigned)(st + bsel + 2) * (BK * 2), a.K - (st + bsel + 2) * BK);
       compute(ima, ima + IMGA);
       as[bsel ^ 1].write(nxt);
       bs[bsel ^ 1].write(nxt + IMGA);

@@ -11,12 +11,15 @@ Same dataclass fields, same call signatures (``(inputs_q, inputs_kv, is_training
 cast to ``dtype`` for compute like Flax's DenseGeneral.  Parameters are created at
 construction when ``in_ch`` is given, otherwise at the first call (Flax ``init`` semantics).
 
-Compute path: projections go through ``ops.dense`` (bf16 forward and input gradient on the
-hand-written ``sae_gemm_nt`` where ``ops.use_gemm_nt`` routes them -- every DeiT-S / CaiT shape --
-the wide ViT-B@384 shapes and the fp32 path on the library GEMM; weight / bias gradients straight
-into fp32 by the split-token MFMA kernel ``sae_gemm_dw``); the self-attention Q/K/V projection is ONE GEMM producing a packed
-[B, N, 3, H, D] buffer that the attention kernel reads in place by strides; the attention core
-is the fused HIP kernel (``ops.attention*``).  There is no eager/CPU fallback.
+Compute path: projections go through ``ops.dense``.  bf16 forward and input gradient run on the
+hand-written ``sae_gemm_nt`` for every width that is a multiple of 8 (the C ABI picks the kernel:
+the persistent LDS-DMA ``gemm8`` for 192-wide output tiles -- every DeiT-S / CaiT shape and the
+ViT-B wide forwards --, the ping-pong ``gemm8x`` for the 768 / 1024-feature outputs at K >= 768,
+the 128-row kernel for the rest, K-tail instances included); the fp32 compute dtype runs on the
+exact-f32 MFMA GEMM ``sae_gemm_f32``; weight / bias gradients go straight into fp32 through the
+split-token MFMA kernels (``sae_gemm_dw``).  The self-attention Q/K/V projection is ONE GEMM
+producing a packed [B, N, 3, H, D] buffer that the attention kernel reads in place by strides; the
+attention core is the fused HIP kernel (``ops.attention*``).  There is no eager/CPU fallback.
 """
 from __future__ import annotations
 

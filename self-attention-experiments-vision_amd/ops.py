@@ -629,8 +629,13 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = No
         raise ValueError(f"gemm_f32: a {tuple(a.shape)} and b {tuple(b.shape)} disagree on K")
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=a.device)
-    elif out.dtype != torch.float32 or tuple(out.shape) != (M, N) or out.stride(1) != 1:
-        raise ValueError(f"gemm_f32: out must be fp32 [{M}, {N}] with unit column stride")
+    elif (out.dtype != torch.float32 or tuple(out.shape) != (M, N) or out.stride(1) != 1
+          or out.device != a.device):
+        raise ValueError(f"gemm_f32: out must be fp32 [{M}, {N}] with unit column stride on {a.device}")
+    if colsum is not None and (colsum.dtype != torch.float32 or colsum.dim() != 1 or colsum.numel() < N
+                               or colsum.stride(0) != 1 or colsum.device != a.device):
+        # the kernel writes colsum[0 .. N) as fp32: anything else would be corrupted silently
+        raise ValueError(f"gemm_f32: colsum must be a unit-stride fp32 vector of >= {N} elements on {a.device}")
     if bias is not None:
         bias = bias.float().contiguous()
     nbytes = lib.sae_gemm_f32_workspace_bytes(M, N, K)
@@ -819,8 +824,10 @@ class _Dense(torch.autograd.Function):
         else:
             # bias rides in the library GEMM's epilogue (addmm) instead of a separate pass
             y = torch.addmm(b.to(dt), x2, wd) if b is not None else x2 @ wd
-        ctx.save_for_backward(x2, wd)
-        ctx.wt = wt   # bf16 W^T [J, I] (the classifier head's input gradient reads it, below)
+        # bf16 W^T [J, I] is kept only for the one input gradient that reads it (below: a small-M
+        # call whose J is not a multiple of 8), through save_for_backward (version-checked)
+        keep_wt = wt is not None and J % 8 != 0 and x2.shape[0] <= SMALL_M
+        ctx.save_for_backward(x2, wd, wt if keep_wt else None)
         ctx.has_b, ctx.xshape, ctx.xdtype = b is not None, x.shape, x.dtype
         ctx.wmeta = [(w.shape[1], w.dtype) for w in ws]
         ctx.sinks_w, ctx.sink_b = [_sink(w) for w in ws], _sink(b)
@@ -829,7 +836,7 @@ class _Dense(torch.autograd.Function):
     @staticmethod
     @_sinking
     def backward(ctx, dy):
-        x2, wd = ctx.saved_tensors
+        x2, wd, wt = ctx.saved_tensors
         I, J = wd.shape
         dy2 = dy.reshape(-1, J)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
@@ -838,13 +845,12 @@ class _Dense(torch.autograd.Function):
             return _Dense._backward_f32(ctx, x2, wd, dy2)
         if use_gemm_nt(J, I) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
-        elif (wd.dtype == torch.bfloat16 and ctx.wt is not None and dy2.shape[0] <= SMALL_M and dy2.shape[0] % 8 == 0
-              and _dw_ok(dy2, ctx.wt)):
-            # K = J not a multiple of 64 (the classifier head: 1000 classes) -- the reduction runs
-            # over the ROWS of dY^T [J, M] and W^T [J, I], i.e. on the weight-gradient kernel:
+        elif (wd.dtype == torch.bfloat16 and wt is not None and dy2.shape[0] % 8 == 0 and _dw_ok(dy2, wt)):
+            # K = J not a multiple of 8 (a classifier head with e.g. 10 classes) -- the reduction
+            # runs over the ROWS of dY^T [J, M] and W^T [J, I], i.e. on the weight-gradient kernel:
             # dx[m][i] = sum_j dY^T[j][m] W^T[j][i], fp32 then the activation dtype
             dxf = torch.empty((dy2.shape[0], I), dtype=torch.float32, device=dy2.device)
-            gemm_dw(dy2.t().contiguous(), ctx.wt, dxf)
+            gemm_dw(dy2.t().contiguous(), wt, dxf)
             dx = dxf.view(ctx.xshape).to(ctx.xdtype)
         else:
             dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
@@ -1003,42 +1009,24 @@ def patch_embed_ok(images: torch.Tensor, w: torch.Tensor, patch: Tuple[int, int]
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 
 
-# sae_gemm_nt vs the library GEMM at the training shapes (tools/gemm_probe.py, tools/nt_probe.py;
-# profiles/r01_gemm_probe_v11.txt, r02_gemm_probe_pin_ab.txt, r03n_nt_probe.txt): the HIP kernel
-# wins for reduction depths <= 384 (DeiT-S QKV forward 35 vs 78 us, output projection 16 vs 24 us)
-# and ties or wins on the narrow (384-feature) input gradients up to K = 1536 (DeiT-S / CaiT QKV
-# dX).  The ViT-B@384 projections stay on the library: in isolation sae_gemm_nt matches it at
-# K = 768 (750-800 TF/s), but in the step (B 32: 870 128 x 128 tiles for the 768-feature
-# outputs, 1.7 rounds over the CUs) the library's 256 x 256 stream-K kernels are faster --
-# same-box A/B (profiles/r03o_vitb_route_ab.txt): every GEMM on sae_gemm_nt 19.0 ms/step, K <= 768
-# on it 18.0, this split 17.8.  GEMM_NT_ALL = True routes everything to sae_gemm_nt (A/B runs).
-GEMM_NT_ALL = False
-GEMM_LIB_WIDE = 0   # A/B switch (tools/ab_knob.py ops.GEMM_LIB_WIDE=v): 1 = round-3 routing (library for K >= 768), 2 = library for the N = 768 outputs only
-GEMM_NT_MAX_K = 512
-SMALL_M = 4096   # Dense calls on at most this many rows (classifier heads, CLS-token projections) always take the HIP GEMMs
-GEMM_NT_NARROW_N = 384
-GEMM_NT_NARROW_MAX_K = 1536
+# Every bf16 forward / input-gradient projection whose widths are multiples of 8 runs on
+# sae_gemm_nt (round 5): the C ABI picks the kernel by tile fill and reduction depth (capi.hip,
+# g8x_route / g8_route: the persistent gemm8, the ping-pong gemm8x, or the 128-row kernel, which
+# also takes K not a multiple of 64).  That covers every width in create_model.py:6-215 (ViT-B/L,
+# DeiT, CaiT 192-768, CeiT, CvT 64/192/368/1024, TNT 24/40/384/640); tests/test_routing_cpu.py
+# pins it.  GEMM_LIB = True sends them to the library GEMM instead (A/B runs only).
+GEMM_LIB = False
+SMALL_M = 4096   # Dense calls on at most this many rows (classifier heads, CLS-token projections)
 
 
 def use_gemm_nt(K: int, N: int) -> bool:
-    """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt.
-    Round 4: the ViT-B shapes go to it as well -- the wide K = 768 outputs (QKV forward, N 2304;
-    FF Dense_0, N 3072) run on the persistent 256-row gemm8 kernel, the 768-feature outputs at
-    K >= 768 (output projection, QKV / Dense_0 input gradients, Dense_1 forward) on the ping-pong
-    gemm8x kernel: 0.90-1.0 of the library there (profiles/r04c_g8probe.txt, r04i_g8probe.txt), and
-    no library GEMM left on the ViT-B@384 path."""
-    base = GEMM_NT_ALL or K <= GEMM_NT_MAX_K or (N <= GEMM_NT_NARROW_N and K <= GEMM_NT_NARROW_MAX_K)
-    if GEMM_LIB_WIDE == 1:
-        return base
-    wide_in = K == 768 and N % 192 == 0 and 1152 <= N <= 3072
-    if GEMM_LIB_WIDE == 2:
-        return base or wide_in
-    return base or wide_in or (N == 768 and K >= 768 and K % 64 == 0)
+    """Route a forward / input-gradient GEMM (reduction depth K, N output features) to sae_gemm_nt."""
+    return not GEMM_LIB and K % 8 == 0 and N % 8 == 0
 
 
 def _nt_ok(a2: torch.Tensor, N: int) -> bool:
     K = a2.shape[1]
-    return (a2.is_cuda and a2.dtype == torch.bfloat16 and K % 64 == 0 and N % 8 == 0 and a2.stride(1) == 1
+    return (a2.is_cuda and a2.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0 and a2.stride(1) == 1
             and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0)
 
 
@@ -1082,12 +1070,9 @@ def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = N
         aux = aux.contiguous()
     if bias is not None:
         bias = bias.float().contiguous()
-    # stream-K shapes (the deep 768-feature outputs) take a workspace for their split tiles
-    nbytes = lib.sae_gemm_nt_workspace_bytes(M, N, K, int(epilogue))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=a2.device) if nbytes else None
-    L.check(lib.sae_gemm_nt_ws(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias),
-                               _ptr(c), c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0,
-                               _ptr(c2), _ptr(ws)))
+    L.check(lib.sae_gemm_nt(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias),
+                            _ptr(c), c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0,
+                            _ptr(c2)))
     return (c, c2) if epilogue == EPI_GELU else c
 
 
@@ -1105,10 +1090,7 @@ class _FFBlock(torch.autograd.Function):
         w0p, w0t = _cast([w0], torch.bfloat16)
         w1p, w1t = _cast([w1], torch.bfloat16)
         a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
-        # Dense_1 forward is a plain GEMM + bias: sae_gemm_nt up to K = hidden 1536 (DeiT-S: 42 vs 44 us for
-        # the library), the library beyond (ViT-B hidden 3072: 82 vs 100 us, profiles/r01_gemm_probe_v13.txt)
-        y = gemm_nt(a, w1t, b1) if Hd <= FF_NT_MAX_HIDDEN or use_gemm_nt(Hd, w1t.shape[0]) else \
-            torch.addmm(b1.to(a.dtype), a, w1p) if b1 is not None else a @ w1p
+        y = gemm_nt(a, w1t, b1)                                   # Dense_1 forward
         ctx.save_for_backward(x2, h, a, w0p, w1p)
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
         ctx.sinks = [_sink(t) for t in (w0, b0, w1, b1)]
@@ -1130,7 +1112,7 @@ class _FFBlock(torch.autograd.Function):
         db1 = _claim(sb1) if sb1 is not None else (
             torch.empty((O,), dtype=torch.float32, device=dev) if ctx.has_b[1] else None)
         gemm_dw(a, dy2, dw1, db1)
-        dx = gemm_nt(dh, w0p) if use_gemm_nt(Hd, I) else dh @ w0p.t()   # dH W0^T
+        dx = gemm_nt(dh, w0p)                                     # dH W0^T
         dw0 = _claim(sw0) if sw0 is not None else torch.empty((I, Hd), dtype=torch.float32, device=dev)
         db0 = _claim(sb0) if sb0 is not None else (
             torch.empty((Hd,), dtype=torch.float32, device=dev) if ctx.has_b[0] else None)
@@ -1140,7 +1122,6 @@ class _FFBlock(torch.autograd.Function):
 
 
 FF_FUSED = True   # tools/ab_step.py flips this to A/B against the library GEMM + torch GELU path
-FF_NT_MAX_HIDDEN = 2048   # Dense_1 forward on sae_gemm_nt up to this reduction depth (hidden width)
 
 
 def ff_block_ok(x: torch.Tensor, w0: torch.Tensor, w1: torch.Tensor) -> bool:
@@ -1148,7 +1129,7 @@ def ff_block_ok(x: torch.Tensor, w0: torch.Tensor, w1: torch.Tensor) -> bool:
         return False
     I, Hd = w0.shape
     O = w1.shape[1]
-    return (x.is_cuda and w0.dtype == w1.dtype == torch.float32 and I % 64 == 0 and Hd % 64 == 0 and O % 8 == 0
+    return (x.is_cuda and w0.dtype == w1.dtype == torch.float32 and I % 8 == 0 and Hd % 8 == 0 and O % 8 == 0
             and w1.shape[0] == Hd)
 
 

@@ -60,6 +60,17 @@ def init_distributed():
     if torch.cuda.is_available():
         local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     world1 = world == 1 and os.environ.get("SAE_WORLD1_RCCL", "0") == "1" and torch.cuda.is_available()
+    if backend == "nccl" or world1:
+        # Peer connections at communicator creation, not at a communicator's first collective:
+        # RCCL (2.26 bundled with torch, 2.27 in /opt/rocm; both read NCCL_RUNTIME_CONNECT) by
+        # default connects the ring / tree peers lazily, inside the first collective that needs
+        # them -- for the gradient group that first collective is issued INSIDE the step's graph
+        # capture (TrainStep._cpg), where the connection setup's allocations and host handshakes
+        # would run in a capturing context.  With 0 every communicator -- the default one created
+        # by init_process_group(device_id=) and the gradient group's by new_group(device_id=) --
+        # is fully connected when its creation returns, so the captured collectives only enqueue
+        # kernels.  A value the user exported wins.
+        os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
     if (world > 1 or world1) and not dist.is_initialized():
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
@@ -79,6 +90,16 @@ def init_distributed():
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
+
+
+def agree_all_ranks(ok: bool, group) -> bool:
+    """True iff ``ok`` holds on every rank of ``group`` (a MIN all-reduce of one flag over a
+    host-side gloo group).  TrainStep decides with it whether the captured graph is used: at
+    world > 1 one rank's capture failure turns the graph off on every rank, so that all ranks
+    issue the same collectives in the same order."""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
 
 
 def flat_layout(params, align: int = 4):
@@ -282,6 +303,10 @@ class TrainStep:
         self._comm_on = True
         if self.collective in ("overlap", "between") and on_gpu:
             self._cpg = dist.new_group(backend="nccl", device_id=params[0].device)
+        # world > 1: whether the step runs as a graph is decided by ALL ranks together (a host-side
+        # gloo group carries the one flag all-reduce): a rank whose capture fails must not run the
+        # eager step while its peers replay graphs -- their collective sequences would differ
+        self._flag_pg = dist.new_group(backend="gloo") if self.world > 1 and self.graph else None
         self.two_graphs = self.collective in ("between", "host") or (self.collective == "none" and bool(two_graphs))
         if self.flat:
             # one flat fp32 gradient buffer, every .grad a 16-byte-aligned view into it (autograd
@@ -564,12 +589,24 @@ class TrainStep:
                 with torch.cuda.graph(go, capture_error_mode=mode):
                     self.opt.step()
                 self._g, self._g_opt = g, go
+            ok = True
         except RuntimeError as e:   # an op that cannot be captured: stay eager, say so once
             import sys
             print(f"[train] HIP-graph capture failed ({e}); running the eager step", file=sys.stderr)
+            ok = False
+        self._settle_capture(ok)
+
+    def _settle_capture(self, ok: bool):
+        """Keep the captured graph(s) or go eager -- at world > 1 on every rank alike (one MIN flag
+        all-reduce over the gloo group): a rank whose capture failed would otherwise run the eager
+        step's collectives while its peers replay graphs."""
+        if self._flag_pg is not None:
+            ok = agree_all_ranks(ok, self._flag_pg)
+        if not ok:
             self.graph = False
             self._g = self._g_opt = None
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
 
     def close(self):
         """Release the captured graphs and the optimizer's persistent bf16 copies.  With a process
@@ -582,9 +619,11 @@ class TrainStep:
         if self.collective == "overlap":
             from . import ops
             ops.set_sink_listener(None)
-        if self._cpg is not None and dist.is_initialized():
-            dist.destroy_process_group(self._cpg)
-            self._cpg = None
+        if dist.is_initialized():
+            for attr in ("_cpg", "_flag_pg"):
+                if getattr(self, attr) is not None:
+                    dist.destroy_process_group(getattr(self, attr))
+                    setattr(self, attr, None)
         if isinstance(self.opt, FusedAdamW):
             self.opt.close()
 

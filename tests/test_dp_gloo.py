@@ -206,3 +206,69 @@ def test_aliased_transform_bucket_waits_for_accumulation(tmp_path):
     finally:
         ops.end_backward_sinks()
         ops.set_grad_sinks(None)
+
+
+def _capture_fail_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from sae_vision_amd import train
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, y = _data()
+    per = x.shape[0] // world
+    step = train.TrainStep(TinyNet(seed=rank), global_batch=x.shape[0], bucket_cap_mb=0.0001)
+    # all ranks captured: the graph stays on everywhere
+    step.graph = True
+    step._flag_pg = dist.new_group(backend="gloo")
+    step._settle_capture(True)
+    both_ok = step.graph
+    # rank 1's capture fails (injected): every rank must turn the graph off, not just rank 1
+    step._settle_capture(rank != 1)
+    after_fail = step.graph
+    # ... and the eager steps that follow stay in lockstep (same collectives on both ranks)
+    for _ in range(2):
+        step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    flat = torch.cat([p.detach().flatten() for p in step.model.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    flags = [None] * world
+    dist.all_gather_object(flags, (both_ok, after_fail))
+    if rank == 0:
+        torch.save({"params": torch.stack(gathered), "flags": flags}, out)
+    step.close()
+    dist.destroy_process_group()
+
+
+def test_capture_failure_on_one_rank_turns_graphs_off_everywhere(tmp_path):
+    """a capture failure at world > 1 is an all-ranks decision (train.py
+    TrainStep._settle_capture: MIN flag all-reduce over a gloo group), never a per-rank eager
+    fallback beside peers that replay graphs."""
+    from sae_vision_amd import train
+    out = str(tmp_path / "capfail.pt")
+    mp.spawn(_capture_fail_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["flags"] == [(True, False), (True, False)], got["flags"]
+    assert torch.equal(got["params"][0], got["params"][1]), "ranks diverged"
+    x, y = _data()
+    ref = train.TrainStep(TinyNet(), global_batch=x.shape[0])
+    for _ in range(2):
+        ref(x, y)
+    flat = torch.cat([p.detach().flatten() for p in ref.model.parameters()])
+    torch.testing.assert_close(got["params"][0], flat, rtol=1e-5, atol=1e-6)
+
+
+def test_init_distributed_connects_eagerly(monkeypatch):
+    """init_distributed asks RCCL for peer connections at communicator
+    creation (NCCL_RUNTIME_CONNECT=0) so the gradient group's first collective -- issued inside the
+    step's graph capture -- does no connection setup there; a user's own setting wins."""
+    from sae_vision_amd import train
+    monkeypatch.delenv("NCCL_RUNTIME_CONNECT", raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("SAE_DIST_BACKEND", "nccl")
+    train.init_distributed()   # world 1, no SAE_WORLD1_RCCL: no process group is created
+    assert os.environ.get("NCCL_RUNTIME_CONNECT") == "0"
+    monkeypatch.setenv("NCCL_RUNTIME_CONNECT", "1")
+    train.init_distributed()
+    assert os.environ["NCCL_RUNTIME_CONNECT"] == "1"
+    assert not dist.is_initialized()

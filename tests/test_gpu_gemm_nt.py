@@ -266,3 +266,54 @@ def test_gemm8_strided(dev):
     ops.gemm_nt(a, bt, out=cw[:, 32:32 + N])
     assert _rel(cw[:, 32:32 + N], a.double() @ bt.double().t()) <= 1e-2
     assert torch.all(cw[:, :32] == 3.0) and torch.all(cw[:, 32 + N:] == 3.0)
+
+
+# Round 5 routing (capi.hip g8x_route / g8_route, sae_gemm_nt_route): K not a multiple of 64 on the
+# 128-row kernel's K-tail instances (CaiT-XXS/XS 288, CvT 368, TNT inner 24 / 40, their FF widths,
+# the classifier head's K = 1000 input gradient), and the ViT-L / CvT-W24 1024 / 4096 widths on
+# gemm8x.  Each case asserts which kernel the C ABI picked, so the test exercises that kernel.
+ROUTE_SHAPES = [  # (M, K, N, epilogue, expected route)
+    (6304, 288, 864, 0, 2), (6304, 864, 288, 0, 2), (6304, 288, 1152, 1, 2), (6304, 288, 1152, 2, 2),
+    (5000, 368, 1104, 0, 2), (5000, 1472, 368, 0, 2), (3136, 40, 120, 0, 2), (3136, 24, 96, 1, 2),
+    (3136, 96, 24, 0, 2), (128, 1000, 384, 0, 2), (197, 40, 40, 2, 2),
+    (18464, 1024, 1024, 0, 4), (18464, 4096, 1024, 0, 4), (9000, 1024, 4096, 1, 4), (9000, 1024, 3072, 0, 3),
+    (6304, 192, 576, 0, 1), (25216, 576, 576, 0, 3),
+]
+
+
+@pytest.mark.parametrize("M,K,N,epi,route", ROUTE_SHAPES)
+def test_gemm_nt_generalised_routes(dev, M, K, N, epi, route):
+    import sae_vision_amd.ops as ops
+    from sae_vision_amd import _lib as L
+    assert L.load().sae_gemm_nt_route(M, N, K, epi) == route
+    a, bt, b = _inputs(dev, M, K, N, 7 * M + K + N)
+    if epi == ops.EPI_GELU:
+        y, h = ops.gemm_nt(a, bt, b, ops.EPI_GELU)
+        assert _rel(h, a.double() @ bt.double().t() + b.double()) <= 1e-2
+        ref_y = F.gelu(h.float(), approximate="tanh")
+        assert float((y.float() - ref_y).abs().max()) <= 2 ** -7 * float(ref_y.abs().max())
+    elif epi == ops.EPI_DGELU:
+        g = torch.Generator(device=dev).manual_seed(5)
+        h = (torch.randn(M, N, device=dev, generator=g) * 2).to(torch.bfloat16)
+        dh = ops.gemm_nt(a, bt, None, ops.EPI_DGELU, aux=h)
+        da = (a.double() @ bt.double().t()).to(torch.bfloat16).float()
+        hf = h.float().requires_grad_(True)
+        F.gelu(hf, approximate="tanh").backward(da)
+        assert _rel(dh, hf.grad) <= 1e-2
+    else:
+        c = ops.gemm_nt(a, bt, b)
+        assert _rel(c, a.double() @ bt.double().t() + b.double()) <= 1e-2
+        assert torch.equal(ops.gemm_nt(a, bt, b), c)
+
+
+def test_gemm_nt_ktail_rowstride(dev):
+    """K-tail kernel reading a row-strided a whose row continues past K (the columns past K of the
+    last stage must read as zero, not as the neighbouring data)."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(9)
+    M, K, N = 3000, 40, 64
+    aw = (torch.randn(M, K + 88, device=dev, generator=g) * 100).to(torch.bfloat16)
+    a = aw[:, :K]
+    bt = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+    c = ops.gemm_nt(a, bt)
+    assert _rel(c, a.double() @ bt.double().t()) <= 1e-2
