@@ -35,10 +35,29 @@ def up_to_date(out=OUT):
     return all(os.path.getmtime(p) <= t for p in deps)
 
 
+def unit_deps(path, seen=None):
+    """The translation unit and every local header it includes (recursively)."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("#include \""):
+            inc = line.split('"')[1]
+            for d in (os.path.dirname(path), os.path.join(ROOT, "include")):
+                if os.path.exists(os.path.join(d, inc)):
+                    unit_deps(os.path.join(d, inc), seen)
+                    break
+    return seen
+
+
 # translation units: (source, extra flags).  capi.hip keeps every MFMA accumulator in VGPRs
 # (-amdgpu-mfma-vgpr-form: the exp / rescale VALU reads them directly); bwd_agpr.hip holds the
-# one-wave-per-SIMD kernels, whose dK / dV accumulators go to the AGPR half of the register file.
-UNITS = [("capi.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd_agpr.hip", [])]
+# one-wave-per-SIMD kernels, whose dK / dV accumulators go to the AGPR half of the register file;
+# attn5.hip / bwd5.hip the round-5 attention kernels (fwd5.h / bwd5.h).
+UNITS = [("capi.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd_agpr.hip", []),
+         ("attn5.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd5.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"])]
 
 
 def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
@@ -55,25 +74,32 @@ def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
         common.append("-DSAE_DEV_KNOBS")
     if stamps:
         common.append("-DSAE_STAMPS")
-    tag = os.path.basename(out).replace(".so", "")
+    tag = os.path.basename(out).replace(".so", "") + ("_g" if debug else "")
+    # objects cached per library flavour: a unit is recompiled only when it or a header it
+    # includes changed (capi.hip takes ~2 minutes; the attention units seconds)
+    objdir = os.path.join(ROOT, "build", tag)
+    os.makedirs(objdir, exist_ok=True)
     objs, procs = [], []
     for src, extra in UNITS:
-        obj = os.path.join(PKG, f".{tag}.{src}.o")
-        cmd = common + extra + ["-c", os.path.join(SRC, src), "-o", obj]
+        path = os.path.join(SRC, src)
+        obj = os.path.join(objdir, src + ".o")
+        objs.append(obj)
+        if not force and os.path.exists(obj) and all(
+                os.path.getmtime(d) <= os.path.getmtime(obj) for d in unit_deps(path)):
+            continue
+        cmd = common + extra + ["-c", path, "-o", obj + ".tmp"]
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-    for p in procs:
+        procs.append((subprocess.Popen(cmd), obj))
+    for p, obj in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, "hipcc")
+        os.replace(obj + ".tmp", obj)
     link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print("[build]", " ".join(link), flush=True)
     subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
-    for o in objs:
-        os.remove(o)
     return out
 
 
