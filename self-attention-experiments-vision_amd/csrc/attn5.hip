@@ -17,11 +17,12 @@ static hipError_t fwd5_run(hipStream_t st, const AttnArgs& a) {
   return hipGetLastError();
 }
 
+template <int PRIO>
 static hipError_t fwd6_run(hipStream_t st, const AttnArgs& a) {
   const long long grid = (long long)((a.Nq + 127) / 128) * a.H * a.B;
   if (grid > 0x7fffffffLL) return hipErrorInvalidConfiguration;
   const size_t lds = 49152;   // 3-deep K / V ring; the final merge image (32 KB + 2 KB)
-  hipLaunchKernelGGL((attn_fwd6_kernel<0>), dim3((unsigned)grid), dim3(512), lds, st, a);
+  hipLaunchKernelGGL((attn_fwd6_kernel<PRIO>), dim3((unsigned)grid), dim3(512), lds, st, a);
   return hipGetLastError();
 }
 
@@ -32,7 +33,8 @@ hipError_t fwd5_launch(hipStream_t st, const AttnArgs& a, int variant) {
     case 1: return d48 ? fwd5_run<4, 2, true, 3>(st, a) : fwd5_run<4, 2, true, 4>(st, a);
     case 2: return d48 ? fwd5_run<4, 3, false, 3>(st, a) : fwd5_run<4, 3, false, 4>(st, a);
     case 3: return d48 ? fwd5_run<8, 1, false, 3>(st, a) : fwd5_run<8, 1, false, 4>(st, a);
-    case 4: return fwd6_run(st, a);
+    case 4: return fwd6_run<0>(st, a);
+    case 5: return fwd6_run<1>(st, a);
     default: return d48 ? fwd5_run<4, 2, false, 3>(st, a) : fwd5_run<4, 2, false, 4>(st, a);
   }
 }

@@ -53,34 +53,44 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
   const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
   const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
 
-  // Q / dO tile t + 1 staged through registers while tile t computes
-  F2Stage<DP, NW> qst, gst;
-  qst.init(tid, a.qs[1], a.D);
-  gst.init(tid, a.dos[1], a.D);
+  // Q / dO tiles staged through registers: NSTG = 1 -- tile t + 1 loaded while tile t computes;
+  // NSTG = 2 (SCHED 2) -- tile t + 2 (two register sets in flight, as bwd2.h)
+  constexpr int NSTG = SCHED == 2 ? 2 : 1;
+  F2Stage<DP, NW> qst[NSTG], gst[NSTG];
+#pragma unroll
+  for (int r = 0; r < NSTG; ++r) {
+    qst[r].init(tid, a.qs[1], a.D);
+    gst[r].init(tid, a.dos[1], a.D);
+  }
   const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
   const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
   const unsigned qstep = (unsigned)(64 * a.qs[1] * 2), gstep = (unsigned)(64 * a.dos[1] * 2);
   const int nqt = (a.Nq + 63) / 64;
-  float rc_l = 0.f, rc_d = 0.f;   // raw row constants of a staged tile (threads 0 .. 63)
-  auto fetch = [&](int qt) {
-    qst.load(rq, (unsigned)qt * qstep);
-    gst.load(rg, (unsigned)qt * gstep);
+  float rc_l[NSTG], rc_d[NSTG];   // raw row constants of a staged tile (threads 0 .. 63)
+#pragma unroll
+  for (int r = 0; r < NSTG; ++r) rc_l[r] = rc_d[r] = 0.f;
+  auto fetch_r = [&](int r, int qt) {
+    qst[r].load(rq, (unsigned)qt * qstep);
+    gst[r].load(rg, (unsigned)qt * gstep);
     if (tid < 64) {
       const int qq = min(qt * 64 + tid, a.Nq - 1);
-      rc_l = a.lse[rowoff + qq];
-      rc_d = a.delta[rowoff + qq];
+      rc_l[r] = a.lse[rowoff + qq];
+      rc_d[r] = a.delta[rowoff + qq];
     }
   };
-  auto put = [&](char* buf, int qt) {
-    qst.write(buf);
-    gst.write(buf + TILE);
+  auto put_r = [&](int r, char* buf, int qt) {
+    qst[r].write(buf);
+    gst[r].write(buf + TILE);
     if (tid < 64) {
       const bool ok = qt * 64 + tid < a.Nq;
-      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = ok ? rc_l * kLog2e : kInf;
-      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = ok ? -rc_d : 0.f;
+      reinterpret_cast<float*>(buf + 2 * TILE)[tid] = ok ? rc_l[r] * kLog2e : kInf;
+      reinterpret_cast<float*>(buf + 2 * TILE + 256)[tid] = ok ? -rc_d[r] : 0.f;
     }
   };
+  auto fetch = [&](int qt) { fetch_r(0, qt); };
+  auto put = [&](char* buf, int qt) { put_r(0, buf, qt); };
   fetch(0);
+  if constexpr (NSTG == 2) fetch_r(1, 1);
 
   bf16x8 kf[NS], vf[NS];
   {
@@ -216,7 +226,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
 #define SAE_FENCE() __builtin_amdgcn_sched_barrier(0)
   auto step_hand = [&](int qt, auto bsel_c) {
     // PROBE (dev timing probes, wrong results): 1 = half 1 reuses half 0's row fragments,
-    // 2 = no lse / -delta reads, 3 = half 1 reuses half 0's transposed fragments
+    // 2 = no lse / -delta reads, 3 = half 1 reuses half 0's transposed fragments, 4 = no global
+    // Q / dO loads (tiles never restaged), 5 = no barrier, 6 = no softmax VALU, 7 = no LDS reads
     constexpr int PROBE = SCHED >= 10 ? SCHED - 10 : 0;
     constexpr int bsel = decltype(bsel_c)::value;
     const char* ldsQ = smem + bsel * TB;
@@ -224,26 +235,37 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
     const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
     const float* ldsD = ldsL + 64;
     char* nxt = smem + (bsel ^ 1) * TB;
-    fetch(qt + 1);
+    if constexpr (PROBE != 4) {
+      if constexpr (NSTG == 2) fetch_r(bsel, qt + 2);   // set bsel went to LDS at the end of tile qt - 1
+      else fetch(qt + 1);
+    }
     SAE_FENCE();
     bf16x8 q0[NS], g0[NS], q1[NS], g1[NS];
     f32x4 l0[4], l1[4];
     f32x16 sp0 = zero16(), dp0, sp1 = zero16(), dp1;
     auto rowrd = [&](int u, int s, bf16x8& qr, bf16x8& gr) {
-      qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
-      gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+      if constexpr (PROBE == 7) {
+        qr = kf[(s + u) & 3];
+        gr = vf[(s + 2 * u) & 3];
+      } else {
+        qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
+        gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+      }
     };
     auto drd = [&](int u, int g, f32x16& dp) {
-      const f32x4 d4 = PROBE == 2 ? f32x4{-0.1f, 0.f, 0.1f, 0.f} : *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
+      const f32x4 d4 = (PROBE == 2 || PROBE == 7) ? f32x4{-0.1f, 0.f, 0.1f, 0.f}
+                                                  : *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
 #pragma unroll
       for (int j = 0; j < 4; ++j) dp[4 * g + j] = d4[j];
     };
     auto lrd = [&](int u, int g, f32x4* l4) {
-      l4[g] = PROBE == 2 ? f32x4{9.f, 9.f, 9.f, 9.f} : *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
+      l4[g] = (PROBE == 2 || PROBE == 7) ? f32x4{9.f, 9.f, 9.f, 9.f}
+                                         : *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h);
     };
     auto sm2 = [&](f32x16& sp, f32x16& dp, const f32x4* l4, int r) {   // two softmax elements r, r + 1
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
+        if constexpr (PROBE == 6) continue;
         const float p = ex2(__builtin_fmaf(sp[r + e], sl2, -l4[(r + e) >> 2][(r + e) & 3]));
         sp[r + e] = p;
         dp[r + e] *= p;
@@ -287,6 +309,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
     //      and transposed reads just ahead of their MFMAs
     bf16x8 tv[2][NT], tq[2][NT];
     auto trd = [&](int u, int s2, int tt, bf16x8& gv, bf16x8& qv) {
+      if constexpr (PROBE == 7) {
+        gv = kf[(s2 + tt + u) & 3];
+        qv = vf[(s2 + 2 * tt + u) & 3];
+        return;
+      }
       const int ro = (32 * u + 16 * s2) * DP * 2;
       gv = tr2(ldsG + ca[2 * tt] + ro, ldsG + ca[2 * tt + 1] + ro);
       qv = tr2(ldsQ + ca[2 * tt] + ro, ldsQ + ca[2 * tt + 1] + ro);
@@ -337,11 +364,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
         SAE_FENCE();
       }
     }
-    put(nxt, qt + 1);
-    __syncthreads();
+    if constexpr (PROBE != 4) {
+      if constexpr (NSTG == 2) put_r(bsel ^ 1, nxt, qt + 1);
+      else put(nxt, qt + 1);
+    }
+    if constexpr (PROBE != 5) __syncthreads();
   };
   auto step = [&](int qt, auto bsel_c) {
-    if constexpr (SCHED == 1 || SCHED >= 10) step_hand(qt, bsel_c);
+    if constexpr (SCHED == 1 || SCHED == 2 || SCHED >= 10) step_hand(qt, bsel_c);
     else step_sgb(qt, bsel_c);
   };
   if (active) {
@@ -355,8 +385,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd5_dkdv_kernel(AttnArgs 
     if (qt < nqt) step(qt, B0{});
   } else {   // waves past the last key only stage tiles and meet the barriers
     for (int qt = 0; qt < nqt; ++qt) {
-      fetch(qt + 1);
-      put(smem + ((qt + 1) & 1) * TB, qt + 1);
+      if constexpr (NSTG == 2) {
+        fetch_r(qt & 1, qt + 2);
+        put_r((qt + 1) & 1, smem + ((qt + 1) & 1) * TB, qt + 1);
+      } else {
+        fetch(qt + 1);
+        put(smem + ((qt + 1) & 1) * TB, qt + 1);
+      }
       __syncthreads();
     }
   }
@@ -388,7 +423,8 @@ namespace sae {
 // written (from registers loaded two phases earlier) at the start of phase 2t + 2, after the last
 // read of tile t - 1, its buffer.  The two groups' dK / dV partials are summed through LDS at the end
 // (fixed order: deterministic).
-template <int DUMMY = 0>
+// PRIO: waves 4-7 (the second-dispatched group, which loses VALU arbitration) at s_setprio 1
+template <int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void attn_bwd6_dkdv_kernel(AttnArgs a) {
   constexpr int DP = 64, NW = 8;
   using FF = F2<DP>;
@@ -560,6 +596,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd6_dkdv_kernel(AttnArgs a) {
   // the same sequence one phase later.  Staging: at the start of every even phase p = 2t + 2 the
   // registers holding tile t + 2 go to the ring and tile t + 3 is fetched.
   const int nph = 2 * nqt + 2;
+  if (PRIO && u == 1) __builtin_amdgcn_s_setprio(1);
   for (int p = 0; p < nph; ++p) {
     if ((p & 1) == 0 && p >= 2) {
       const int t = p / 2 - 1;   // p = 2t + 2
@@ -622,7 +659,8 @@ namespace sae {
 // delta = rowsum(dO o O) is formed from the fragments in registers and published for the dK / dV
 // pass; -delta and -lse2 are per-lane constants (the query is on the lane): -delta is the dP^T
 // MFMAs' initial accumulator.  The groups' dQ partials are summed through LDS at the end.
-template <int DUMMY = 0>
+// PRIO: waves 4-7 (the second-dispatched group, which loses VALU arbitration) at s_setprio 1
+template <int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void attn_bwd6_dq_kernel(AttnArgs a) {
   constexpr int DP = 64, NW = 8;
   using FF = F2<DP>;
@@ -771,6 +809,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd6_dq_kernel(AttnArgs a) {
     for (int s2 = 0; s2 < 2; ++s2) sf[s2] = acc_frag<__bf16>(dp, s2);
   };
   const int nph = 2 * nkt + 2;
+  if (PRIO && u == 1) __builtin_amdgcn_s_setprio(1);
   for (int p = 0; p < nph; ++p) {
     if ((p & 1) == 0 && p >= 2) {
       const int t = p / 2 - 1;
@@ -806,6 +845,265 @@ __global__ __launch_bounds__(512, 1) void attn_bwd6_dq_kernel(AttnArgs a) {
     const int q0 = qb * BQ + qg * 32;
     __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hh * a.dqs[2] + (long long)q0 * a.dqs[1];
     wave_store_rows<DP>(adq, a.scale, smem + qg * 32 * DP * 2, DQ, a.dqs[1], a.Nq - q0, a.D, lane);
+  }
+}
+
+}  // namespace sae
+
+namespace sae {
+
+// one 1-KiB LDS-DMA piece (16 bytes per lane at LDS byte address lds + 16 lane; M0 saved and
+// restored inside the statement, as gemm8.h g8_dma1) and the 256-byte dword form
+__device__ __forceinline__ void b7_dma16(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void b7_dma4(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+template <int N> __device__ __forceinline__ void b7_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// --------------------------------------------- dK / dV pass, LDS-DMA staged, hand-ordered body
+// As attn_bwd5_dkdv_kernel (SCHED 1: both query halves of a 64-query tile in one hand-ordered
+// block), with the Q / dO tiles and their row constants staged by LDS-DMA into a 3-deep ring:
+// tile t + 2 is issued at the top of tile t (its buffer held tile t - 1, whose readers all passed
+// the barrier that ended tile t - 1), and the counted vmcnt + barrier at the end of tile t makes
+// tile t + 1 visible -- two tiles of load latency hidden, no staging registers, no ds_write.  The
+// row constants come ready from the dQ pass (attn_bwd2_dq_kernel PUB2: -delta, lse log2 e); query
+// rows past Nq read as zeros (range check), which leaves their dS and their dV / dK terms zero.
+// The DMA writes lane-linearly: the XOR swizzle of the tile images goes into the source address.
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void attn_bwd7_dkdv_kernel(AttnArgs a) {
+  constexpr int DP = 64, NW = 4;
+  using FF = F2<DP>;
+  constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
+  constexpr int BK = 32 * NW;
+  constexpr int TB = 2 * TILE + 2 * 64 * 4;   // [Q img | dO img | lse2[64] | -delta[64]]
+  constexpr int NBUF = 3;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nkb = (a.Nk + BK - 1) / BK;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = bid % nkb;
+  bid /= nkb;
+  const int hh = bid % a.H;
+  const int b = bid / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int key = kb * BK + w * 32 + r32;
+  const bool active = kb * BK + w * 32 < a.Nk;
+  const size_t rowoff = ((size_t)b * a.H + hh) * a.Nq;
+
+  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + hh * a.qs[2];
+  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + hh * a.ks[2];
+  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + hh * a.vs[2];
+  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + hh * a.dos[2];
+  const __amdgpu_buffer_rsrc_t rq = row_rsrc(Q, a.Nq, a.qs[1]);
+  const __amdgpu_buffer_rsrc_t rg = row_rsrc(G, a.Nq, a.dos[1]);
+  const __amdgpu_buffer_rsrc_t rdl = row_rsrc(a.delta + rowoff, a.Nq, 1);   // -delta
+  const __amdgpu_buffer_rsrc_t rl2 = row_rsrc(a.delta + (size_t)a.B * a.H * a.Nq + rowoff, a.Nq, 1);   // lse log2 e
+  const int nqt = (a.Nq + 63) / 64;
+  const unsigned lbase = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+  // this wave's pieces: Q / dO rows 8p .. 8p + 7 for p = w, w + 4; lane L: row 8p + L / 8, image
+  // chunk L % 8 = global chunk (L % 8) ^ swz(row) (chunks past the head dim read zero)
+  unsigned goq[2], gog[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (w + 4 * i) + (lane >> 3);
+    const int c = (lane & 7) ^ swz<DP>(row);
+    const bool ok = c * 8 < a.D;
+    goq[i] = ok ? (unsigned)(((long long)row * a.qs[1] + 8 * c) * 2) : 0x80000000u;
+    gog[i] = ok ? (unsigned)(((long long)row * a.dos[1] + 8 * c) * 2) : 0x80000000u;
+  }
+  const unsigned qstep = (unsigned)(64 * a.qs[1] * 2), gstep = (unsigned)(64 * a.dos[1] * 2);
+  // pieces per tile: 4 per wave, + the lse2 piece (wave 0) / the -delta piece (wave 1)
+  auto issue = [&](int t) {
+    const unsigned lb = lbase + (unsigned)((t % NBUF) * TB);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const unsigned p = (unsigned)(w + 4 * i) * 1024u;
+      b7_dma16(rq, goq[i] + (unsigned)t * qstep, lb + p);
+      b7_dma16(rg, gog[i] + (unsigned)t * gstep, lb + TILE + p);
+    }
+    if (w == 0) b7_dma4(rl2, (unsigned)(t * 64 + lane) * 4u, lb + 2 * TILE);
+    if (w == 1) b7_dma4(rdl, (unsigned)(t * 64 + lane) * 4u, lb + 2 * TILE + 256);
+  };
+  // wait for tile t (all older pieces; the pieces of tile t + 1 may stay in flight) + barrier
+  auto wait_tile = [&](bool next_in_flight) {
+    if (next_in_flight) {
+      if (w < 2) b7_wait_barrier<5>(); else b7_wait_barrier<4>();
+    } else {
+      b7_wait_barrier<0>();
+    }
+  };
+
+  bf16x8 kf[NS], vf[NS];
+  {
+    const __amdgpu_buffer_rsrc_t rk = row_rsrc(K, a.Nk, a.ks[1]);
+    const __amdgpu_buffer_rsrc_t rv = row_rsrc(V, a.Nk, a.vs[1]);
+    const unsigned ko = (unsigned)((long long)key * a.ks[1] * 2);
+    const unsigned vo = (unsigned)((long long)key * a.vs[1] * 2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      const bool ok = d0 < a.D;
+      kf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, ok ? ko + d0 * 2 : 0x80000000u, 0, 0));
+      vf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, ok ? vo + d0 * 2 : 0x80000000u, 0, 0));
+    }
+  }
+  vm_wait_all();   // K / V fragments resident (the waitcnt pass cannot see the asm DMA)
+  issue(0);
+  if (nqt > 1) issue(1);
+  wait_tile(nqt > 1);
+
+  const float sl2 = a.scale * kLog2e;
+  unsigned ra[NS], ca[2 * NT];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) ra[s] = r32 * DP * 2 + 16 * ((2 * s + h) ^ swz<DP>(r32));
+  {
+    const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int colb = 32 * t + 16 * (g & 1) + 4 * (li & 3);
+      const int chunk = colb >> 3, half = (colb >> 2) & 1;
+      const int r1 = 4 * h + (li >> 2), r2 = r1 + 8;
+      ca[2 * t] = r1 * DP * 2 + 16 * (chunk ^ swz<DP>(r1)) + 8 * half;
+      ca[2 * t + 1] = r2 * DP * 2 + 16 * (chunk ^ swz<DP>(r2)) + 8 * half;
+    }
+  }
+  f32x16 adk[NT], adv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    adk[t] = zero16();
+    adv[t] = zero16();
+  }
+
+#define SAE_FENCE7() __builtin_amdgcn_sched_barrier(0)
+  for (int qt = 0; qt < nqt; ++qt) {
+    if (qt + 2 < nqt) issue(qt + 2);
+    SAE_FENCE7();
+    if (active) {
+      const char* ldsQ = smem + (qt % NBUF) * TB;
+      const char* ldsG = ldsQ + TILE;
+      const float* ldsL = reinterpret_cast<const float*>(ldsQ + 2 * TILE);
+      const float* ldsD = ldsL + 64;
+      bf16x8 q0[NS], g0[NS], q1[NS], g1[NS];
+      f32x4 l0[4], l1[4];
+      f32x16 sp0 = zero16(), dp0, sp1 = zero16(), dp1;
+      auto rowrd = [&](int u, int s, bf16x8& qr, bf16x8& gr) {
+        qr = *reinterpret_cast<const bf16x8*>(ldsQ + ra[s] + 32 * u * DP * 2);
+        gr = *reinterpret_cast<const bf16x8*>(ldsG + ra[s] + 32 * u * DP * 2);
+      };
+      auto drd = [&](int u, int g, f32x16& dp) {
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ldsD + 32 * u + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dp[4 * g + j] = d4[j];
+      };
+      auto lrd = [&](int u, int g, f32x4* l4) { l4[g] = *reinterpret_cast<const f32x4*>(ldsL + 32 * u + 8 * g + 4 * h); };
+      auto sm2 = [&](f32x16& sp, f32x16& dp, const f32x4* l4, int r) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float p = ex2(__builtin_fmaf(sp[r + e], sl2, -l4[(r + e) >> 2][(r + e) & 3]));
+          sp[r + e] = p;
+          dp[r + e] *= p;
+        }
+      };
+#pragma unroll
+      for (int g = 0; g < 4; ++g) drd(0, g, dp0);
+      rowrd(0, 0, q0[0], g0[0]);
+      rowrd(0, 1, q0[1], g0[1]);
+      SAE_FENCE7();
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {   // segment 0: S0 / dP0
+        sp0 = MF<__bf16>::mma(q0[s], kf[s], sp0);
+        if (s + 2 < NS) rowrd(0, s + 2, q0[s + 2], g0[s + 2]);
+        else { lrd(0, 2 * (s - 2), l0); lrd(0, 2 * (s - 2) + 1, l0); }
+        SAE_FENCE7();
+        dp0 = MF<__bf16>::mma(g0[s], vf[s], dp0);
+        if (s < 2) { drd(1, 2 * s, dp1); drd(1, 2 * s + 1, dp1); }
+        else rowrd(1, s - 2, q1[s - 2], g1[s - 2]);
+        SAE_FENCE7();
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {   // segment 1: S1 / dP1 beside half 0's softmax
+        sp1 = MF<__bf16>::mma(q1[s], kf[s], sp1);
+        if (s + 2 < NS) rowrd(1, s + 2, q1[s + 2], g1[s + 2]);
+        sm2(sp0, dp0, l0, 4 * s);
+        SAE_FENCE7();
+        dp1 = MF<__bf16>::mma(g1[s], vf[s], dp1);
+        if (s >= 2) { lrd(1, 2 * (s - 2), l1); lrd(1, 2 * (s - 2) + 1, l1); }
+        sm2(sp0, dp0, l0, 4 * s + 2);
+        SAE_FENCE7();
+      }
+      bf16x8 tv[2][NT], tq[2][NT];
+      auto trd = [&](int u, int s2, int tt, bf16x8& gv, bf16x8& qv) {
+        const int ro = (32 * u + 16 * s2) * DP * 2;
+        gv = tr2(ldsG + ca[2 * tt] + ro, ldsG + ca[2 * tt + 1] + ro);
+        qv = tr2(ldsQ + ca[2 * tt] + ro, ldsQ + ca[2 * tt + 1] + ro);
+      };
+      trd(0, 0, 0, tv[0][0], tq[0][0]);
+      trd(0, 0, 1, tv[0][1], tq[0][1]);
+      bf16x8 pf = acc_frag<__bf16>(sp0, 0), sf = acc_frag<__bf16>(dp0, 0);
+      SAE_FENCE7();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {   // segment 2: half 0's dV / dK beside half 1's softmax
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+          adv[tt] = MF<__bf16>::mma(tv[s2][tt], pf, adv[tt]);
+          if (s2 == 0) trd(0, 1, tt, tv[1][tt], tq[1][tt]);
+          sm2(sp1, dp1, l1, 8 * s2 + 4 * tt);
+          SAE_FENCE7();
+          adk[tt] = MF<__bf16>::mma(tq[s2][tt], sf, adk[tt]);
+          sm2(sp1, dp1, l1, 8 * s2 + 4 * tt + 2);
+          SAE_FENCE7();
+        }
+        if (s2 == 0) {
+          pf = acc_frag<__bf16>(sp0, 1);
+          sf = acc_frag<__bf16>(dp0, 1);
+          SAE_FENCE7();
+        }
+      }
+      trd(1, 0, 0, tv[0][0], tq[0][0]);
+      trd(1, 0, 1, tv[0][1], tq[0][1]);
+      pf = acc_frag<__bf16>(sp1, 0);
+      sf = acc_frag<__bf16>(dp1, 0);
+      SAE_FENCE7();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {   // segment 3: half 1's dV / dK
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+          adv[tt] = MF<__bf16>::mma(tv[s2][tt], pf, adv[tt]);
+          if (s2 == 0) trd(1, 1, tt, tv[1][tt], tq[1][tt]);
+          SAE_FENCE7();
+          adk[tt] = MF<__bf16>::mma(tq[s2][tt], sf, adk[tt]);
+          SAE_FENCE7();
+        }
+        if (s2 == 0) {
+          pf = acc_frag<__bf16>(sp1, 1);
+          sf = acc_frag<__bf16>(dp1, 1);
+          SAE_FENCE7();
+        }
+      }
+    }
+    // tile qt + 1 landed (the pieces of qt + 2 may stay in flight) and every wave done with qt
+    if (qt + 1 < nqt) wait_tile(qt + 2 < nqt);
+    else b7_wait_barrier<0>();
+  }
+  if (active) {
+    const int k0 = kb * BK + w * 32;
+    char* scr = smem + w * 32 * DP * 2;
+    __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + hh * a.dks[2] + (long long)k0 * a.dks[1];
+    __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + hh * a.dvs[2] + (long long)k0 * a.dvs[1];
+    wave_store_rows<DP>(adk, a.scale, scr, DK, a.dks[1], a.Nk - k0, a.D, lane);
+    wave_store_rows<DP>(adv, 1.f, scr, DV, a.dvs[1], a.Nk - k0, a.D, lane);
   }
 }
 

@@ -232,7 +232,7 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
   if constexpr (DP == 64 && !ROT) {
     // fwd5 (one basic block per full tile, pre-scaled queries, -max as the score MFMAs' initial
     // accumulator); dev builds: SAE_FWD_VARIANT 20-23 select its forms
-    if (var >= 20 && var <= 24) {   // measured slower than fwd2 (profiles/r05b_attn_ab.txt): dev only
+    if (var >= 20 && var <= 25) {   // measured slower than fwd2 (profiles/r05b_attn_ab.txt): dev only
       const hipError_t e = fwd5_launch(st, a, var - 20);
       if (e != hipSuccess) return fail(SAE_EHIP, "attn_fwd5: launch failed: %s", hipGetErrorString(e));
       return ok();
@@ -301,7 +301,8 @@ namespace sae {
 hipError_t bwd2_dkdv_agpr(hipStream_t st, const AttnArgs& a, int dp, bool pipe);   // bwd_agpr.hip
 hipError_t bwd2_agpr128(hipStream_t st, const AttnArgs& a, bool rel, int variant);  // bwd_agpr.hip
 hipError_t bwd5_dkdv_launch(hipStream_t st, const AttnArgs& a, int variant);       // bwd5.hip
-hipError_t bwd6_dq_launch(hipStream_t st, const AttnArgs& a);                       // bwd5.hip
+hipError_t bwd6_dq_launch(hipStream_t st, const AttnArgs& a, int prio);             // bwd5.hip
+hipError_t bwd7_launch(hipStream_t st, const AttnArgs& a, int variant);             // bwd5.hip
 }
 namespace {
 
@@ -309,8 +310,13 @@ namespace {
 // hand-ordered basic block)
 template <int DP> int bwd5_run(hipStream_t st, const AttnArgs& a, int variant) {
   static_assert(DP == 64, "bwd5: head_dim <= 64");
-  if (variant >= 8) {   // ping-pong dQ pass (8: + ping-pong dK / dV, 9: + bwd2-style dK / dV)
-    const hipError_t e = bwd6_dq_launch(st, a);
+  if (variant == 15 || variant == 16) {   // LDS-DMA staged dK / dV (bwd7), 16: one wave per SIMD
+    const hipError_t e = bwd7_launch(st, a, variant == 16 ? 1 : 0);
+    if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd7: %s", hipGetErrorString(e));
+    return ok();
+  }
+  if (variant >= 8 && variant <= 10) {   // ping-pong dQ pass; 8: + ping-pong dK / dV, 9: + bwd2 dK / dV, 10: both at setprio
+    const hipError_t e = bwd6_dq_launch(st, a, variant == 10);
     if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd6_dq: %s", hipGetErrorString(e));
     if (variant == 9) {
       const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512);
@@ -318,7 +324,7 @@ template <int DP> int bwd5_run(hipStream_t st, const AttnArgs& a, int variant) {
       hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, 4, 2>), dim3((unsigned)grid), dim3(256), lds, st, a);
       return check_launch("attn_bwd2_dkdv");
     }
-    const hipError_t e2 = bwd5_dkdv_launch(st, a, 7);
+    const hipError_t e2 = bwd5_dkdv_launch(st, a, variant == 10 ? 8 : 7);
     if (e2 != hipSuccess) return fail(SAE_EHIP, "attn_bwd6_dkdv: %s", hipGetErrorString(e2));
     return ok();
   }
@@ -790,7 +796,7 @@ static size_t delta_bytes(const sae_attn_desc* d) {
 
 size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
   if (!d) return 0;
-  return delta_bytes(d);
+  return 2 * delta_bytes(d);   // delta [B, H, Nq] (+ lse * log2 e for the round-5 dK / dV pass)
 }
 
 static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
@@ -879,7 +885,7 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     if (dp == 64 && (var == 10 || var == 11)) return bwd2_run_agpr<64>(st, a, var == 11);
     // key ranges > 256 at head_dim <= 64 (ViT-B/16@384): the round-5 dK / dV pass; dev builds:
     // SAE_BWD_VARIANT 19 = the round-4 bwd2 pair, 20-23 the bwd5 forms, 24-26 timing probes
-    if (dp == 64 && var >= 20 && var <= 29) return bwd5_run<64>(st, a, var - 20);
+    if (dp == 64 && var >= 20 && var <= 39) return bwd5_run<64>(st, a, var - 20);
 #endif
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);

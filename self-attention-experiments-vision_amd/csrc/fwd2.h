@@ -35,6 +35,13 @@ __device__ __forceinline__ float xhalf_max(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// pairwise sum of the 16 accumulator values of a 32 x 32 tile
+__device__ __forceinline__ float f2_tree16(const f32x16& x) {
+  const float a0 = (x[0] + x[1]) + (x[2] + x[3]), a1 = (x[4] + x[5]) + (x[6] + x[7]);
+  const float a2 = (x[8] + x[9]) + (x[10] + x[11]), a3 = (x[12] + x[13]) + (x[14] + x[15]);
+  return (a0 + a1) + (a2 + a3);
+}
+
 __device__ __forceinline__ float xhalf_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -213,13 +220,10 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
     for (int r = 0; r < 16; ++r) s1[r] = ex2(__builtin_fmaf(s1[r], sl2, -m));
   }
   if constexpr (!LSUM) {
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ls += s0[r];
-    if (two) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ls += s1[r];
-    }
+    // pairwise (depth 4 per half): a serial chain of 32 dependent adds sat on the tile's critical
+    // path (round-5 ISA of the N = 577 instance)
+    float ls = f2_tree16(s0);
+    if (two) ls += f2_tree16(s1);
     l = FIRST ? ls : l + ls;
   }
   bf16x8 ones;

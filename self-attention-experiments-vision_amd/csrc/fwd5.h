@@ -288,7 +288,8 @@ namespace sae {
 // m = max(m0, m1), O = O0 2^(m0 - m) + O1 2^(m1 - m), l likewise.  A row whose sum left [1, 2^64)
 // in either group (a later score far above its first tile's max) makes the workgroup redo the sweep
 // with per-tile max tracking (TRACK).
-template <int DUMMY = 0>
+// PRIO: waves 4-7 (the second-dispatched group, which loses VALU arbitration) at s_setprio 1
+template <int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void attn_fwd6_kernel(AttnArgs a) {
   constexpr int DP = 64, NW = 8;
   using FF = F2<DP>;
@@ -439,6 +440,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd6_kernel(AttnArgs a) {
       for (int s2 = 0; s2 < 2; ++s2) pf[s2] = acc_frag<__bf16>(sp, s2);
     };
     const int nph = 2 * nkt + 2;
+    if (PRIO && u == 1) __builtin_amdgcn_s_setprio(1);
     for (int p = 0; p < nph; ++p) {
       if ((p & 1) == 0 && p >= 2) {
         const int t = p / 2 - 1;
