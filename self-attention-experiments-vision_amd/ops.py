@@ -16,6 +16,7 @@ Public functions
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 from typing import Optional, Tuple
@@ -24,7 +25,7 @@ import torch
 
 from . import _lib as L
 
-__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "cast_weights", "clear_weight_cache", "gemm_dw", "layer_norm", "add_layer_norm", "add_layer_norm_scaled", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
+__all__ = ["attention", "attention_packed", "dense", "ff_block", "gemm_nt", "weight_cast", "cast_weights", "clear_weight_cache", "gemm_dw", "set_weight_grad_stream", "join_weight_grad_stream", "layer_norm", "add_layer_norm", "add_layer_norm_scaled", "layer_norm_ok", "talking_heads_attention", "talking_heads_attention_packed", "relpos_bias", "rotary",
            "rotary_tables", "dtype_code", "KernelTimer", "set_kernel_timer"]
 
 
@@ -74,8 +75,13 @@ def _sinking(bwd):
             done = _CLAIM_LOG[n0:]
             del _CLAIM_LOG[n0:]
             if _SINK_LISTENER is not None:
-                for ptr in done:
-                    _SINK_LISTENER(ptr)
+                if _WG_STREAM is not None:
+                    # a sink may have been written on the weight-gradient stream: the listener's
+                    # collective waits on that stream, which first picks up the main stream's work
+                    _WG_STREAM.wait_stream(torch.cuda.current_stream(_WG_STREAM.device))
+                with torch.cuda.stream(_WG_STREAM) if _WG_STREAM is not None else contextlib.nullcontext():
+                    for ptr in done:
+                        _SINK_LISTENER(ptr)
         return out
     return wrapped
 
@@ -592,25 +598,53 @@ def _claim(sink: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 # ------------------------------------------------------------------------------ projections
+# Side stream of the weight-gradient GEMMs (set_weight_grad_stream): inside the training step's
+# sink window, a weight gradient that goes into a sink is off the backward's critical path, so its
+# GEMM runs on this stream beside the input-gradient chain (LayerNorm / attention backward and the
+# next dX GEMM) instead of between them; the step joins it before the optimizer.
+_WG_STREAM = None
+
+
+def set_weight_grad_stream(stream) -> None:
+    """Run the sink-bound weight-gradient GEMMs of the following backwards on ``stream`` (None:
+    on the current stream).  The caller joins it with :func:`join_weight_grad_stream`."""
+    global _WG_STREAM
+    _WG_STREAM = stream
+
+
+def join_weight_grad_stream() -> None:
+    """Make the current stream wait for every weight-gradient GEMM enqueued on the side stream."""
+    if _WG_STREAM is not None:
+        torch.cuda.current_stream(_WG_STREAM.device).wait_stream(_WG_STREAM)
+
+
 def gemm_dw(x2: torch.Tensor, dy2: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor] = None,
-            accumulate: bool = False, jblock: int = 0) -> None:
+            accumulate: bool = False, jblock: int = 0, offload: bool = False) -> None:
     """dw (+)= x2^T dy2 and db (+)= colsum(dy2) in fp32 through ``sae_gemm_dw`` (split over the
     token axis, fixed-order reduction).  x2 [M, I], dy2 [M, J] bf16 with unit column stride.
-    ``jblock`` > 0: dw is [J / jblock, I, jblock] (contiguous column blocks)."""
+    ``jblock`` > 0: dw is [J / jblock, I, jblock] (contiguous column blocks).  ``offload``: dw / db
+    are gradient sinks nobody reads before the step's join, so the GEMM may run on the
+    weight-gradient side stream (when one is set and the sink window is open)."""
     lib = L.load()
     _require_gpu(x2, dy2, dw)
     M, I = x2.shape
     J = dy2.shape[1]
-    ws = torch.empty(lib.sae_gemm_dw_workspace_bytes(M, I, J), dtype=torch.uint8, device=x2.device)
-    tok = _TIMER.begin("gemm_dw") if _TIMER is not None else None
-    if jblock:
-        L.check(lib.sae_gemm_dw_blocked(_stream(x2), M, I, J, int(jblock), _ptr(x2), x2.stride(0), _ptr(dy2),
-                                        dy2.stride(0), _ptr(dw), _ptr(db), int(accumulate), _ptr(ws)))
-    else:
-        L.check(lib.sae_gemm_dw(_stream(x2), M, I, J, _ptr(x2), x2.stride(0), _ptr(dy2), dy2.stride(0), _ptr(dw),
-                                dw.stride(0), _ptr(db), int(accumulate), _ptr(ws)))
-    if tok is not None:
-        _TIMER.end(tok, (M, I, J))
+    side = _WG_STREAM if (offload and _SINK_WINDOW and _WG_STREAM is not None) else None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(x2.device))   # x2 / dy2 are written on the main stream
+        x2.record_stream(side)    # ... and stay allocated until the side stream has read them
+        dy2.record_stream(side)
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        ws = torch.empty(lib.sae_gemm_dw_workspace_bytes(M, I, J), dtype=torch.uint8, device=x2.device)
+        tok = _TIMER.begin("gemm_dw") if _TIMER is not None else None
+        if jblock:
+            L.check(lib.sae_gemm_dw_blocked(_stream(x2), M, I, J, int(jblock), _ptr(x2), x2.stride(0), _ptr(dy2),
+                                            dy2.stride(0), _ptr(dw), _ptr(db), int(accumulate), _ptr(ws)))
+        else:
+            L.check(lib.sae_gemm_dw(_stream(x2), M, I, J, _ptr(x2), x2.stride(0), _ptr(dy2), dy2.stride(0),
+                                    _ptr(dw), dw.stride(0), _ptr(db), int(accumulate), _ptr(ws)))
+        if tok is not None:
+            _TIMER.end(tok, (M, I, J))
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -869,13 +903,14 @@ class _Dense(torch.autograd.Function):
                                           for k, t in enumerate(sw)):   # adjacent sinks: one [nb, I, n] block
                     for t in sw:
                         _claim(t)
-                    gemm_dw(x2, dy2, s0.as_strided((len(widths), I, n), (I * n, n, 1)), db, jblock=n)
+                    gemm_dw(x2, dy2, s0.as_strided((len(widths), I, n), (I * n, n, 1)), db, jblock=n,
+                            offload=sb is not None or not ctx.has_b)
                     return (dx, rdb, None, *[None] * len(widths))
                 dwb = torch.empty((len(widths), I, n), dtype=torch.float32, device=x2.device)
                 gemm_dw(x2, dy2, dwb, db, jblock=n)
                 return (dx, rdb, None, *[dwb[k].to(wdt) for k, (_, wdt) in enumerate(ctx.wmeta)])
             if sw[0] is not None:
-                gemm_dw(x2, dy2, _claim(sw[0]), db)
+                gemm_dw(x2, dy2, _claim(sw[0]), db, offload=sb is not None or not ctx.has_b)
                 return dx, rdb, None, None
             dw = torch.empty((I, J), dtype=torch.float32, device=x2.device)
             gemm_dw(x2, dy2, dw, db)
@@ -1111,12 +1146,12 @@ class _FFBlock(torch.autograd.Function):
         dw1 = _claim(sw1) if sw1 is not None else torch.empty((Hd, O), dtype=torch.float32, device=dev)
         db1 = _claim(sb1) if sb1 is not None else (
             torch.empty((O,), dtype=torch.float32, device=dev) if ctx.has_b[1] else None)
-        gemm_dw(a, dy2, dw1, db1)
+        gemm_dw(a, dy2, dw1, db1, offload=sw1 is not None and (sb1 is not None or not ctx.has_b[1]))
         dx = gemm_nt(dh, w0p)                                     # dH W0^T
         dw0 = _claim(sw0) if sw0 is not None else torch.empty((I, Hd), dtype=torch.float32, device=dev)
         db0 = _claim(sb0) if sb0 is not None else (
             torch.empty((Hd,), dtype=torch.float32, device=dev) if ctx.has_b[0] else None)
-        gemm_dw(x2, dh, dw0, db0)
+        gemm_dw(x2, dh, dw0, db0, offload=sw0 is not None and (sb0 is not None or not ctx.has_b[0]))
         ret = [None if sk is not None else g for sk, g in zip(ctx.sinks, (dw0, db0, dw1, db1))]
         return (dx.view(ctx.xshape).to(ctx.xdtype), *ret)
 

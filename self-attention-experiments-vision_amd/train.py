@@ -266,7 +266,8 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, global_batch: int, lr: float = 5e-4, weight_decay: float = 1e-4,
                  label_smoothing: float = 0.1, bucket_cap_mb: float = 25.0, device: Optional[torch.device] = None,
                  graph: bool = False, input_layout: str = "NHWC", flat_grads: Optional[bool] = None,
-                 grad_sinks: bool = True, two_graphs: Optional[bool] = None, persistent_casts: bool = True):
+                 grad_sinks: bool = True, two_graphs: Optional[bool] = None, persistent_casts: bool = True,
+                 wgrad_stream: Optional[bool] = None):
         # input_layout "HWCN": the batch arrives as the reference's train-step feed [H, W, C, N]
         # (train.py:80, input_pipeline.py:187-191) and the model's patch GEMM gathers from it
         self.input_layout = input_layout
@@ -341,6 +342,14 @@ class TrainStep:
                 ops.set_grad_sinks(params, [p.grad for p in params])
             if self.collective == "overlap":
                 self._arm_overlap_hooks()
+        # the sink-bound weight-gradient GEMMs run on a side stream beside the input-gradient chain
+        # (ops.set_weight_grad_stream), opt-in: SAE_WG_STREAM=1 or wgrad_stream=True.  Off by default: the
+        # concurrent dW kernels push the persistent gemm8 tiles into a tail (DeiT-S 15,381 vs
+        # 15,619 img/s, profiles/r05i_wgstream_rejected.txt)
+        if wgrad_stream is None:
+            wgrad_stream = os.environ.get("SAE_WG_STREAM", "0") == "1"
+        self._wg = (torch.cuda.Stream(device=params[0].device)
+                    if wgrad_stream and self.flat and self._sinks and on_gpu else None)
         base_lr = lr * (global_batch / 512)
         kw = dict(lr=base_lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         self.opt = None
@@ -479,6 +488,7 @@ class TrainStep:
         overlap = self.collective == "overlap"
         if sinks:
             ops.begin_backward_sinks()   # the sink window: this step's forward + backward only
+            ops.set_weight_grad_stream(self._wg)
         try:
             if overlap:
                 self._begin_overlap()
@@ -490,11 +500,14 @@ class TrainStep:
             # world > 1: the SUM all-reduce of the per-rank gradients of loss / world is the
             # gradient of the global-batch mean (survey D9)
             (loss / self.world if self.world > 1 else loss).backward()
+            if sinks:
+                ops.join_weight_grad_stream()   # every weight gradient written before the update
             if overlap:
                 self._end_overlap()
         finally:
             if sinks:
                 ops.end_backward_sinks()
+                ops.set_weight_grad_stream(None)
             if overlap:
                 self._armed = False
         if sinks and self.graph and not torch.cuda.is_current_stream_capturing():

@@ -26,6 +26,10 @@ SHAPES = {  # name: (B, Nq, Nk, H, D)
     "bot7": (256, 49, 49, 4, 128),
     "cvt1": (64, 3136, 784, 1, 64),
     "cait_m24": (128, 196, 196, 16, 48),
+    # the per-workgroup work of a key-split single-pass backward at the ViT-B/16@384 headline
+    # (same query x key products as vitb384): 3 key ranges of 192 or 2.25 of 256
+    "vb_k192": (192, 577, 192, 12, 64),
+    "vb_k256": (144, 577, 256, 12, 64),
 }
 
 
