@@ -452,36 +452,38 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
   return check_launch("th_reduce");
 }
 
-// bf16 with the head mixes on the MFMA (th2.h); NWMAX = 8 or 16 waves per workgroup
-template <int DP, int NWMAX, bool ROT> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
-  const int nqb = (a.Nq + 31) / 32;
-  const size_t lds = th2_lds_bytes<DP, NWMAX <= 8>(a.H);
-  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT>, lds)) return rc;
-  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+// bf16 with the head mixes on the MFMA (th2.h).  H <= 8: one wave per head (NWMAX 8).  9..16 heads:
+// two heads per wave (eight waves of <= 256 registers; sixteen waves of 128 spilled heavily).
+template <int DP, int NWMAX, bool ROT, int HPW> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
+  const int nqb = (a.Nq + 31) / 32, nw = (a.H + HPW - 1) / HPW;
+  const size_t lds = th2_lds_bytes<DP, NWMAX * HPW <= 8>(a.H);
+  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW>, lds)) return rc;
+  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   return check_launch("th2_fwd");
 }
 
-template <int DP, int NWMAX, bool ROT> int th2_bwd_run(hipStream_t st, ThArgs a) {
-  const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32;
+template <int DP, int NWMAX, bool ROT, int HPW> int th2_bwd_run(hipStream_t st, ThArgs a) {
+  constexpr bool KST = NWMAX * HPW <= 8;
+  const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32, nw = (a.H + HPW - 1) / HPW;
   a.nblk = nqb * a.B;
-  const size_t lds = th2_lds_bytes<DP, NWMAX <= 8>(a.H), lds_kv = th2_kv_lds_bytes<DP, NWMAX <= 8>(a.H, NWMAX <= 8);
-  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT>, lds)) return rc;
-  if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT>, lds_kv)) return rc;
-  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT>), dim3(nqb * a.B), dim3(64 * a.H), lds, st, a);
+  const size_t lds = th2_lds_bytes<DP, KST>(a.H, HPW), lds_kv = th2_kv_lds_bytes<DP, KST>(a.H, KST);
+  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>, lds)) return rc;
+  if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT, HPW>, lds_kv)) return rc;
+  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   if (int rc = check_launch("th2_bwd_q")) return rc;
-  hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX, ROT>), dim3(nkb * a.B), dim3(64 * a.H), lds_kv, st, a);
+  hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX, ROT, HPW>), dim3(nkb * a.B), dim3(64 * nw), lds_kv, st, a);
   if (int rc = check_launch("th2_bwd_kv")) return rc;
   hipLaunchKernelGGL(th_reduce_kernel, dim3(2 * a.H * a.H), dim3(256), 0, st, a);
   return check_launch("th_reduce");
 }
 
 template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
-  if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true>(st, a) : th2_fwd_run<DP, 16, true>(st, a);
-  return a.H <= 8 ? th2_fwd_run<DP, 8, false>(st, a) : th2_fwd_run<DP, 16, false>(st, a);
+  if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true, 1>(st, a) : th2_fwd_run<DP, 8, true, 2>(st, a);
+  return a.H <= 8 ? th2_fwd_run<DP, 8, false, 1>(st, a) : th2_fwd_run<DP, 8, false, 2>(st, a);
 }
 template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
-  if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true>(st, a) : th2_bwd_run<DP, 16, true>(st, a);
-  return a.H <= 8 ? th2_bwd_run<DP, 8, false>(st, a) : th2_bwd_run<DP, 16, false>(st, a);
+  if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true, 1>(st, a) : th2_bwd_run<DP, 8, true, 2>(st, a);
+  return a.H <= 8 ? th2_bwd_run<DP, 8, false, 1>(st, a) : th2_bwd_run<DP, 8, false, 2>(st, a);
 }
 
 }  // namespace

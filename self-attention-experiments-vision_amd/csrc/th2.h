@@ -188,8 +188,9 @@ __device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// sum of per-wave 16 x 16 partials (one per wave, in LDS scratch) -> this workgroup's dT slot
-__device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* out, int H, int w, int lane,
+// sum of per-wave 16 x 16 partials (one per wave of the NW, in LDS scratch) -> this workgroup's dT
+// slot (the first 256 threads: NW >= 4 when H > 4)
+__device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* out, int H, int NW, int w, int lane,
                                              int tid, bool transpose_out) {
   // acc[j] = dT[h = 4 (lane >> 4) + j][i = lane & 15]
   f32x4* s4 = reinterpret_cast<f32x4*>(scratch);
@@ -198,7 +199,7 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
   if (tid < 256) {
     const int ln = tid & 63, j = tid >> 6;   // element j of lane ln: h = 4 (ln >> 4) + j, i = ln & 15
     float s = 0.f;
-    for (int ww = 0; ww < H; ++ww) s += scratch[(ww * 64 + ln) * 4 + j];
+    for (int ww = 0; ww < NW; ++ww) s += scratch[(ww * 64 + ln) * 4 + j];
     const int h = 4 * (ln >> 4) + j, i = ln & 15;
     if (h < H && i < H) out[transpose_out ? i * H + h : h * H + i] = s;
   }
@@ -209,42 +210,54 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
 // (Measured and dropped: double-buffered images with the next tile's scores issued before this
 // tile's mixes and one barrier per tile -- 238 vs 221 us at cait_s24: in-order issue stalls on
 // the score tile's MFMA results before the mixes can start, so nothing overlapped.)
-template <int DP, int NWMAX, bool ROT = false>
+// HPW heads per wave (1, or 2 for 9..16 heads: eight waves of up to 256 registers instead of
+// sixteen of 128, which spilled); wave w owns heads w + NW e, e < HPW, NW = ceil(H / HPW) waves.
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
 __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
-  constexpr bool KST = NWMAX <= 8;           // H <= 8: stacked mixes, heads in registers 0..3
+  constexpr bool KST = NWMAX * HPW <= 8;     // H <= 8: stacked mixes, heads in registers 0..3
   constexpr int NR = KST ? 4 : 8;            // registers r < NR hold the mixed heads row_of(r, h)
   constexpr int IMG = th2_img<KST>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H;
+  const int H = a.H, NW = (H + HPW - 1) / HPW;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* const XS = smem;                    // scores S_h (bf16), then statistics scratch
   char* const XP = smem + IMG;              // mixed probabilities P2_j (bf16)
-  char* ldsV = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
   // XCD-aware order: the query blocks of one image run on one XCD and share its K / V in L2
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = lb % nqb, b = lb / nqb;
   const int q = qb * 32 + r32;
-  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
-  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
-  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
-  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
-                               rV = row_rsrc(V, a.Nk, a.vs[1]);
+  int hd[HPW];                              // this wave's heads (hd[e] >= H: none, e > 0 only)
+  bool hv[HPW];
+  char* ldsV[HPW];
+  __amdgpu_buffer_rsrc_t rQ[HPW], rK[HPW], rV[HPW];
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    hd[e] = w + NW * e;
+    hv[e] = hd[e] < H;
+    const int he = hv[e] ? hd[e] : w;
+    ldsV[e] = smem + 2 * IMG + he * I::bytes(32);
+    rQ[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + he * a.qs[2], a.Nq, a.qs[1]);
+    rK[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + he * a.ks[2], a.Nk, a.ks[1]);
+    rV[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + he * a.vs[2], a.Nk, a.vs[1]);
+  }
 
-  th2_zero_pad<KST>(XS, H, tid, 64 * H);
-  th2_zero_pad<KST>(XP, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * NW);
+  th2_zero_pad<KST>(XP, H, tid, 64 * NW);
   constexpr bool rot = ROT;   // rotary: q / k rotated as they are loaded
   const bool full = a.D > 16 * (NS - 1);   // the last 16-wide k-step holds head-dim columns
-  bf16x8 qf[NS];
+  bf16x8 qf[HPW][NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    qf[s] = th2_frag(rQ, q, a.qs[1], a.D, s, h);
-    if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
-  }
+  for (int e = 0; e < HPW; ++e)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[e][s] = th2_frag(rQ[e], q, a.qs[1], a.D, s, h);
+      if (rot) qf[e][s] = rope8<1>(qf[e][s], a.rope, q, 16 * s + 8 * h);
+    }
   const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);   // S1 = T1^T S
   const Th2Mix m2 = th2_mix<false, true, KST>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
   const int nkt = (a.Nk + 31) / 32;
@@ -259,30 +272,37 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   }
   // K fragments of the next key tile are loaded while this one computes (the global latency
   // would otherwise sit in front of every tile's first MFMA)
+  // one head per wave: the next key tile's K fragments are in flight while this one computes; two
+  // heads: the registers hold the second head's Q instead and each head's K loads directly
+  constexpr bool PF = HPW == 1;
   bf16x8 kn[NS];
-  auto load_k = [&](int kt) {
+  auto load_k = [&](int e, int kt) {
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) kn[s_] = th2_frag(rK, kt * 32 + r32, a.ks[1], a.D, s_, h);
+    for (int s_ = 0; s_ < NS; ++s_) kn[s_] = th2_frag(rK[e], kt * 32 + r32, a.ks[1], a.D, s_, h);
   };
   auto scores = [&](int kt) {
-    bf16x8 kc[NS];
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
-    load_k(kt + 1 < nkt ? kt + 1 : 0);
-    f32x16 s = zero16();
+    for (int e = 0; e < HPW; ++e) {
+      if constexpr (!PF) load_k(e, kt);
+      bf16x8 kc[NS];
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_)
-      if (s_ < NS - 1 || full) s = MF<__bf16>::mma(qf[s_], kc[s_], s);   // S^T: query rows, key lanes
-    th2_put(XS, w, s, a.scale, lane);
+      for (int s_ = 0; s_ < NS; ++s_) kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
+      if constexpr (PF) load_k(0, kt + 1 < nkt ? kt + 1 : 0);
+      f32x16 s = zero16();
+#pragma unroll
+      for (int s_ = 0; s_ < NS; ++s_)
+        if (s_ < NS - 1 || full) s = MF<__bf16>::mma(qf[e][s_], kc[s_], s);   // S^T: query rows, key lanes
+      if (hv[e]) th2_put(XS, hd[e], s, a.scale, lane);
+    }
   };
   auto stats = [&](int kt) {   // this wave's blocks of tile kt, groups of four: one max update each
     const char* xs = XS;
-    for (int b0 = w; b0 < 32; b0 += 4 * H) {
+    for (int b0 = w; b0 < 32; b0 += 4 * NW) {
       f32x16 c[4];
       bool ok[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {   // independent chains: issued together, blocks past the end clamped
-        const int blk = b0 + u * H;
+        const int blk = b0 + u * NW;
         ok[u] = blk < 32 && kt * 32 + blk < a.Nk;
         c[u] = th2_mix_img<KST>(xs, blk & 31, m1, lane);
       }
@@ -303,7 +323,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       }
     }
   };
-  load_k(0);
+  if constexpr (PF) load_k(0, 0);
   for (int kt = 0; kt < nkt; ++kt) {
     scores(kt);
     __syncthreads();
@@ -319,7 +339,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       float mm = -kInf, ll = 0.f;
-      for (int ww = 0; ww < H; ++ww) {
+      for (int ww = 0; ww < NW; ++ww) {
         const float2 v = st[(ww * NR + r) * 64 + lane];
         const float mn = fmaxf(mm, v.x);
         ll = (mm == -kInf ? 0.f : ll * ex2(mm - mn)) + (v.x == -kInf ? 0.f : v.y * ex2(v.x - mn));
@@ -331,25 +351,27 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       if (w == 0 && i < H && q < a.Nq) a.lse[((size_t)b * H + i) * a.Nq + q] = (mm + lg2(ll)) * kLn2;
     }
     __syncthreads();
-    th2_zero_pad<KST>(XS, H, tid, 64 * H);   // the scratch overwrote the pad rows
-    th2_zero_pad<KST>(XP, H, tid, 64 * H);
+    th2_zero_pad<KST>(XS, H, tid, 64 * NW);   // the scratch overwrote the pad rows
+    th2_zero_pad<KST>(XP, H, tid, 64 * NW);
   }
 
   // ---- pass 1: P_i = 2^(S1 - m) / l, P2 = T2^T P into XP, O_w += P2_w V_w
-  f32x16 acco[NT];
+  f32x16 acco[HPW][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acco[t] = zero16();
+  for (int e = 0; e < HPW; ++e)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acco[e][t] = zero16();
   auto probs = [&](int kt) {   // this wave's blocks of tile kt: P2 = T2^T P into XP
     const char* xs = XS;
     char* xp = XP;
     constexpr int G = KST ? 4 : 2;   // blocks per group: independent chains issued together
-    for (int b0 = w; b0 < 32; b0 += G * H) {
+    for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 c[G];
 #pragma unroll
-      for (int u = 0; u < G; ++u) c[u] = th2_mix_img<KST>(xs, (b0 + u * H) & 31, m1, lane);
+      for (int u = 0; u < G; ++u) c[u] = th2_mix_img<KST>(xs, (b0 + u * NW) & 31, m1, lane);
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        const int blk = b0 + u * H;
+        const int blk = b0 + u * NW;
         const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: P = 0
 #pragma unroll
         for (int r = 0; r < NR; ++r) c[u][r] = ok ? ex2(__builtin_fmaf(c[u][r], kLog2e, -m[r])) * l[r] : 0.f;
@@ -361,85 +383,122 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < G; ++u)
-        if (b0 + u * H < 32) th2_put_block<NR>(xp, b0 + u * H, c[u], H, lane);
+        if (b0 + u * NW < 32) th2_put_block<NR>(xp, b0 + u * NW, c[u], H, lane);
     }
   };
   auto pv = [&]() {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = th2_colB(XP, w, s2, lane);
+    for (int e = 0; e < HPW; ++e)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acco[t] = MF<__bf16>::mma(I::colfrag(ldsV, 0, s2, 32 * t, lane), pf, acco[t]);
-    }
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = th2_colB(XP, hv[e] ? hd[e] : w, s2, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acco[e][t] = MF<__bf16>::mma(I::colfrag(ldsV[e], 0, s2, 32 * t, lane), pf, acco[e][t]);
+      }
   };
-  WStage<__bf16, DP, true> vst;   // V tile kt + 1 in flight while tile kt computes (wave-private image)
-  vst.load_buf(rV, 0, a.vs[1], a.D, lane);
-  vst.write(ldsV, lane);
+  WStage<__bf16, DP, true> vst[HPW];   // V tile kt + 1 in flight while tile kt computes (wave-private images)
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    vst[e].load_buf(rV[e], 0, a.vs[1], a.D, lane);
+    vst[e].write(ldsV[e], lane);
+  }
   for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vst.load_buf(rV, (kt + 1) * 32, a.vs[1], a.D, lane);
+    if (kt + 1 < nkt)
+#pragma unroll
+      for (int e = 0; e < HPW; ++e) vst[e].load_buf(rV[e], (kt + 1) * 32, a.vs[1], a.D, lane);
     scores(kt);
     __syncthreads();
     probs(kt);
     __syncthreads();
     pv();
-    if (kt + 1 < nkt) vst.write(ldsV, lane);   // wave-private: after this wave's own reads
+    if (kt + 1 < nkt)   // wave-private: after this wave's own reads
+#pragma unroll
+      for (int e = 0; e < HPW; ++e) vst[e].write(ldsV[e], lane);
     __syncthreads();
   }
   if (q < a.Nq) {
-    __bf16* O = reinterpret_cast<__bf16*>(a.o) + b * a.os[0] + w * a.os[2] + (long long)q * a.os[1];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int e = 0; e < HPW; ++e) {
+      if (!hv[e]) continue;
+      __bf16* O = reinterpret_cast<__bf16*>(a.o) + b * a.os[0] + hd[e] * a.os[2] + (long long)q * a.os[1];
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        store4<__bf16, true>(O, 32 * t + 8 * g + 4 * h, a.D, acco[t][4 * g], acco[t][4 * g + 1], acco[t][4 * g + 2],
-                             acco[t][4 * g + 3]);
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          store4<__bf16, true>(O, 32 * t + 8 * g + 4 * h, a.D, acco[e][t][4 * g], acco[e][t][4 * g + 1],
+                               acco[e][t][4 * g + 2], acco[e][t][4 * g + 3]);
+    }
   }
 }
 
 // ============================================================================ bwd: query
 // pass A: delta_i = rowsum(P_i o dP_i), dP = T2 dP2, dP2_j = dO_j V_j^T; dT2 = sum P (x) dP2.
 // pass B: dS1 = P o (dP - delta), dT1 = sum S (x) dS1, dS = T1 dS1, dQ_w += scale dS_w K_w.
-template <int DP, int NWMAX, bool ROT = false>
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
-  constexpr bool KST = NWMAX <= 8;
+  constexpr bool KST = NWMAX * HPW <= 8;
   constexpr int NR = KST ? 4 : 8;
   constexpr int IMG = th2_img<KST>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H;
+  const int H = a.H, NW = (H + HPW - 1) / HPW;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* XS = smem;
   char* XG = smem + IMG;
-  char* ldsK = smem + 2 * IMG + w * I::bytes(32);
 
   const int nqb = (a.Nq + 31) / 32;
   // XCD-aware order: the query blocks of one image run on one XCD and share its K / V in L2
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = lb % nqb, b = lb / nqb;
   const int q = qb * 32 + r32;
-  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
-  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
-  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
-  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
-  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
-                               rV = row_rsrc(V, a.Nk, a.vs[1]), rG = row_rsrc(G, a.Nq, a.dos[1]);
+  int hd[HPW];                              // this wave's heads (as th2_fwd_kernel)
+  bool hv[HPW];
+  char* ldsK[HPW];
+  __amdgpu_buffer_rsrc_t rQ[HPW], rK[HPW], rV[HPW], rG[HPW];
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    hd[e] = w + NW * e;
+    hv[e] = hd[e] < H;
+    const int he = hv[e] ? hd[e] : w;
+    ldsK[e] = smem + 2 * IMG + he * I::bytes(32);
+    rQ[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + he * a.qs[2], a.Nq, a.qs[1]);
+    rK[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + he * a.ks[2], a.Nk, a.ks[1]);
+    rV[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + he * a.vs[2], a.Nk, a.vs[1]);
+    rG[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + he * a.dos[2], a.Nq, a.dos[1]);
+  }
 
-  th2_zero_pad<KST>(XS, H, tid, 64 * H);
-  th2_zero_pad<KST>(XG, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * NW);
+  th2_zero_pad<KST>(XG, H, tid, 64 * NW);
   constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dq rotated back
   const bool full = a.D > 16 * (NS - 1);
-  bf16x8 qf[NS], gf[NS];
+  bf16x8 qf[HPW][NS], gf[HPW][NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    qf[s] = th2_frag(rQ, q, a.qs[1], a.D, s, h);
-    if (rot) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
-    gf[s] = th2_frag(rG, q, a.dos[1], a.D, s, h);
+  for (int e = 0; e < HPW; ++e)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[e][s] = th2_frag(rQ[e], q, a.qs[1], a.D, s, h);
+      if (rot) qf[e][s] = rope8<1>(qf[e][s], a.rope, q, 16 * s + 8 * h);
+      gf[e][s] = th2_frag(rG[e], q, a.dos[1], a.D, s, h);
+    }
+  // the mix operands: registers (one head per wave) or, with two heads per wave, an LDS table that
+  // wave 0 writes before the first barrier (the registers go to the second head's operands)
+  Th2Mix m1r, m2tr, m1tr;
+  Th2Mix* const mxt = reinterpret_cast<Th2Mix*>(smem + 2 * IMG + H * I::bytes(32));
+  if constexpr (HPW == 1) {
+    m1r = th2_mix<false, false, KST>(a.th1, H, lane);    // S1 = T1^T S        (image)
+    m2tr = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
+    m1tr = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
+  } else if (w == 0) {
+    mxt[lane] = th2_mix<false, false, KST>(a.th1, H, lane);
+    mxt[64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);
+    mxt[128 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);
   }
-  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);    // S1 = T1^T S        (image)
-  const Th2Mix m2t = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
-  const Th2Mix m1t = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
+  auto m1 = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1r; else return mxt[lane]; };
+  auto m2t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m2tr; else return mxt[64 + lane]; };
+  auto m1t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1tr; else return mxt[128 + lane]; };
   // lse (log2 domain) of the mixed rows of this lane's query, register r <-> head row_of(r, h)
   float lse2[NR];
 #pragma unroll
@@ -448,34 +507,49 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     lse2[r] = (i < H && q < a.Nq) ? a.lse[((size_t)b * H + i) * a.Nq + q] * kLog2e : kInf;
   }
   const int nkt = (a.Nk + 31) / 32;
-  bf16x8 kn[NS], vn[NS];   // next key tile's K / V fragments, in flight while this one computes
-  auto load_kv = [&](int kt) {
+  // next key tile's K / V fragments, in flight while this one computes (one head per wave: with
+  // two, the registers go to the second head's operands instead and the loads are direct)
+  constexpr bool PF = HPW == 1;
+  bf16x8 kn[NS], vn[NS];
+  auto load_kv = [&](int e, int kt) {
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
-      kn[s_] = th2_frag(rK, kt * 32 + r32, a.ks[1], a.D, s_, h);
-      vn[s_] = th2_frag(rV, kt * 32 + r32, a.vs[1], a.D, s_, h);
+      kn[s_] = th2_frag(rK[e], kt * 32 + r32, a.ks[1], a.D, s_, h);
+      vn[s_] = th2_frag(rV[e], kt * 32 + r32, a.vs[1], a.D, s_, h);
     }
   };
-  auto tiles = [&](int kt) {   // S_w -> XS, dP2_w -> XG
-    bf16x8 kc[NS], vc[NS];
+  // S_h -> XS, dP2_h -> XG for this wave's heads; stage_k: the (rotated) K fragments also form the
+  // head's K image, the dQ product's operand (key rows, the WStage layout)
+  auto tiles = [&](int kt, bool stage_k) {
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) {
-      kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
-      vc[s_] = vn[s_];
-    }
-    load_kv(kt + 1 < nkt ? kt + 1 : 0);
-    f32x16 s = zero16(), g = zero16();
+    for (int e = 0; e < HPW; ++e) {
+      if constexpr (!PF) load_kv(e, kt);
+      bf16x8 kc[NS], vc[NS];
 #pragma unroll
-    for (int s_ = 0; s_ < NS; ++s_) {
-      if (s_ < NS - 1 || full) {   // S^T, dP2^T: query rows, key lanes
-        s = MF<__bf16>::mma(qf[s_], kc[s_], s);
-        g = MF<__bf16>::mma(gf[s_], vc[s_], g);
+      for (int s_ = 0; s_ < NS; ++s_) {
+        kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
+        vc[s_] = vn[s_];
+      }
+      if constexpr (PF) load_kv(0, kt + 1 < nkt ? kt + 1 : 0);
+      if (stage_k)
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_)
+          *reinterpret_cast<bf16x8*>(ldsK[e] + r32 * (DP * 2) + 16 * ((2 * s_ + h) ^ swz<DP>(r32))) = kc[s_];
+      f32x16 s = zero16(), g = zero16();
+#pragma unroll
+      for (int s_ = 0; s_ < NS; ++s_) {
+        if (s_ < NS - 1 || full) {   // S^T, dP2^T: query rows, key lanes
+          s = MF<__bf16>::mma(qf[e][s_], kc[s_], s);
+          g = MF<__bf16>::mma(gf[e][s_], vc[s_], g);
+        }
+      }
+      if (hv[e]) {
+        th2_put(XS, hd[e], s, a.scale, lane);
+        th2_put(XG, hd[e], g, 1.f, lane);
       }
     }
-    th2_put(XS, w, s, a.scale, lane);
-    th2_put(XG, w, g, 1.f, lane);
   };
-  load_kv(0);
+  if constexpr (PF) load_kv(0, 0);
 
   // ---- pass A
   float dl[NR];
@@ -483,19 +557,19 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   for (int r = 0; r < NR; ++r) dl[r] = 0.f;
   f32x4 dt2 = {0.f, 0.f, 0.f, 0.f};
   for (int kt = 0; kt < nkt; ++kt) {
-    tiles(kt);
+    tiles(kt, false);
     __syncthreads();
     constexpr int G = 2;   // blocks per group: independent chains issued together
-    for (int b0 = w; b0 < 32 && kt * 32 + b0 < a.Nk; b0 += G * H) {
+    for (int b0 = w; b0 < 32 && kt * 32 + b0 < a.Nk; b0 += G * NW) {
       f32x16 p[G], dp[G];
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        p[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, m1, lane);
-        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, m2t, lane);
+        p[u] = th2_mix_img<KST>(XS, (b0 + u * NW) & 31, m1(), lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * NW) & 31, m2t(), lane);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        const int blk = b0 + u * H;
+        const int blk = b0 + u * NW;
         const bool ok = blk < 32 && kt * 32 + blk < a.Nk;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -519,7 +593,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       float s = 0.f;
-      for (int ww = 0; ww < H; ++ww) s += st[(ww * NR + r) * 64 + lane];
+      for (int ww = 0; ww < NW; ++ww) s += st[(ww * NR + r) * 64 + lane];
       dl[r] = s;
       const int i = row_of(r, h);
       if (w == 0 && i < H && q < a.Nq) a.delta[((size_t)b * H + i) * a.Nq + q] = s;
@@ -527,33 +601,31 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     __syncthreads();
   }
   float* pb = a.part + (size_t)blockIdx.x * 2 * H * H;
-  th2_dt_store(reinterpret_cast<float*>(smem), dt2, pb + H * H, H, w, lane, tid, false);
-  th2_zero_pad<KST>(XS, H, tid, 64 * H);
-  th2_zero_pad<KST>(XG, H, tid, 64 * H);   // (the last tile of pass A prefetched key tile 0)
+  th2_dt_store(reinterpret_cast<float*>(smem), dt2, pb + H * H, H, NW, w, lane, tid, false);
+  th2_zero_pad<KST>(XS, H, tid, 64 * NW);
+  th2_zero_pad<KST>(XG, H, tid, 64 * NW);   // (the last tile of pass A prefetched key tile 0)
 
   // ---- pass B
-  f32x16 adq[NT];
+  f32x16 adq[HPW][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) adq[t] = zero16();
+  for (int e = 0; e < HPW; ++e)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) adq[e][t] = zero16();
   f32x4 dt1 = {0.f, 0.f, 0.f, 0.f};
-  WStage<__bf16, DP, true> kst;
   for (int kt = 0; kt < nkt; ++kt) {
-    kst.load_buf(rK, kt * 32, a.ks[1], a.D, lane);
-    tiles(kt);
-    if (rot) kst.rope(a.rope, kt * 32, lane);
-    kst.write(ldsK, lane);
+    tiles(kt, true);   // (wave-private K images: after this wave's previous dQ reads)
     __syncthreads();
-    constexpr int G = 2;
-    for (int b0 = w; b0 < 32; b0 += G * H) {
+    constexpr int G = HPW == 1 ? 2 : 1;   // (two heads per wave: one chain, the registers are short)
+    for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 ds1[G], dp[G];
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        ds1[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, m1, lane);
-        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, m2t, lane);
+        ds1[u] = th2_mix_img<KST>(XS, (b0 + u * NW) & 31, m1(), lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * NW) & 31, m2t(), lane);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        const int blk = b0 + u * H;
+        const int blk = b0 + u * NW;
         const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: dS = 0
 #pragma unroll
         for (int r = 0; r < NR; ++r)
@@ -565,35 +637,42 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
         if (blk < 32) {
           th2_put_block<NR>(XG, blk, ds1[u], H, lane);   // dS1 over dP2 at this block
           if (ok) dt1 = th2_dt<KST>(XS, XG, blk, dt1, lane);   // dT1[h][i] += sum S_h dS1_i
-          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(ds1[u], m1t), H, lane);   // dS_h over S_h
+          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(ds1[u], m1t()), H, lane);   // dS_h over S_h
         }
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 sf = th2_colB(XS, w, s2, lane);
+    for (int e = 0; e < HPW; ++e)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) adq[t] = MF<__bf16>::mma(I::colfrag(ldsK, 0, s2, 32 * t, lane), sf, adq[t]);
-    }
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 sf = th2_colB(XS, hv[e] ? hd[e] : w, s2, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          adq[e][t] = MF<__bf16>::mma(I::colfrag(ldsK[e], 0, s2, 32 * t, lane), sf, adq[e][t]);
+      }
     __syncthreads();
   }
   // dT1 partial: XS held the SCALED scores (S = scale q k, the reference's logits)
-  th2_dt_store(reinterpret_cast<float*>(smem), dt1, pb, H, w, lane, tid, false);
+  th2_dt_store(reinterpret_cast<float*>(smem), dt1, pb, H, NW, w, lane, tid, false);
   if (q < a.Nq) {
-    __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + w * a.dqs[2] + (long long)q * a.dqs[1];
     const float sc = a.scale;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int e = 0; e < HPW; ++e) {
+      if (!hv[e]) continue;
+      __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hd[e] * a.dqs[2] + (long long)q * a.dqs[1];
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * t + 8 * g4 + 4 * h;
-        float x[4];
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[e] = (float)(__bf16)(adq[t][4 * g4 + e] * sc);
-        if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, q, d0 / 2);
-        store4<__bf16, true>(DQ, d0, a.D, x[0], x[1], x[2], x[3]);
-      }
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * t + 8 * g4 + 4 * h;
+          float x[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[c] = (float)(__bf16)(adq[e][t][4 * g4 + c] * sc);
+          if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, q, d0 / 2);
+          store4<__bf16, true>(DQ, d0, a.D, x[0], x[1], x[2], x[3]);
+        }
+    }
   }
 }
 
@@ -602,44 +681,64 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 // (same mixes), dV_w^T += dO_w^T P2_w, dK_w^T += scale Q_w^T dS_w.  The score tiles keep the key
 // on the accumulator rows and the query on the lane, so image position = key * 32 + query and the
 // per-head operands read query runs of a key: plain 16-byte row reads.
-template <int DP, int NWMAX, bool ROT = false>
+// HPW = 2 (9..16 heads, eight waves of <= 256 registers): each wave keeps the dK / dV accumulators
+// of its two heads; the key block's K / V fragments are re-read per query tile (L2-resident, 4 KiB
+// per head) instead of held, and the dO / Q tiles go through one staging buffer per head.
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
-  constexpr bool KST = NWMAX <= 8;
+  constexpr bool KST = NWMAX * HPW <= 8;
   constexpr int NR = KST ? 4 : 8;
   constexpr int IMG = th2_img<KST>();
+  constexpr bool KVR = HPW == 1;   // K / V fragments held in registers for the whole sweep
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H;
+  const int H = a.H, NW = (H + HPW - 1) / HPW;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* XS = smem;
   char* XG = smem + IMG;
   char* MX = smem + 2 * IMG;   // the four mix operands, per lane (registers are short here)
-  char* buf = MX + kTh2MixTbl + w * I::bytes(32);
 
   const int nkb = (a.Nk + 31) / 32;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);   // the key blocks of one image on one XCD
   const int kb = lb % nkb, b = lb / nkb;
   const int key = kb * 32 + r32;
-  const __bf16* Q = reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + w * a.qs[2];
-  const __bf16* K = reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + w * a.ks[2];
-  const __bf16* V = reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + w * a.vs[2];
-  const __bf16* G = reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + w * a.dos[2];
-  const __amdgpu_buffer_rsrc_t rQ = row_rsrc(Q, a.Nq, a.qs[1]), rK = row_rsrc(K, a.Nk, a.ks[1]),
-                               rV = row_rsrc(V, a.Nk, a.vs[1]), rG = row_rsrc(G, a.Nq, a.dos[1]);
+  // per-wave dO / Q tiles: with <= 8 heads both images stay resident (the S / dP2 operands are read
+  // from them and the next tile is in flight during this one); otherwise one 4 KiB buffer per head
+  // (dO for dV, then Q for dK) and the S / dP2 operands come from global memory
+  constexpr bool TWO = NWMAX * HPW <= 8;
+  int hd[HPW];
+  bool hv[HPW];
+  char *buf[HPW], *bufQ[HPW];
+  __amdgpu_buffer_rsrc_t rQ[HPW], rK[HPW], rV[HPW], rG[HPW];
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    hd[e] = w + NW * e;
+    hv[e] = hd[e] < H;
+    const int he = hv[e] ? hd[e] : w;
+    buf[e] = MX + kTh2MixTbl + he * I::bytes(32);
+    bufQ[e] = TWO ? buf[e] + NWMAX * I::bytes(32) : buf[e];
+    rQ[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.q) + b * a.qs[0] + he * a.qs[2], a.Nq, a.qs[1]);
+    rK[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.k) + b * a.ks[0] + he * a.ks[2], a.Nk, a.ks[1]);
+    rV[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.v) + b * a.vs[0] + he * a.vs[2], a.Nk, a.vs[1]);
+    rG[e] = row_rsrc(reinterpret_cast<const __bf16*>(a.dout) + b * a.dos[0] + he * a.dos[2], a.Nq, a.dos[1]);
+  }
 
-  th2_zero_pad<KST>(XS, H, tid, 64 * H);
-  th2_zero_pad<KST>(XG, H, tid, 64 * H);
+  th2_zero_pad<KST>(XS, H, tid, 64 * NW);
+  th2_zero_pad<KST>(XG, H, tid, 64 * NW);
   constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dk rotated back
   const bool full = a.D > 16 * (NS - 1);
-  bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block
+  bf16x8 kf[NS], vf[NS];   // A operands: key rows of this block (KVR: loaded once)
+  auto load_kv = [&](int e) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    kf[s] = th2_frag(rK, key, a.ks[1], a.D, s, h);
-    if (rot) kf[s] = rope8<1>(kf[s], a.rope, key, 16 * s + 8 * h);
-    vf[s] = th2_frag(rV, key, a.vs[1], a.D, s, h);
-  }
+    for (int s_ = 0; s_ < NS; ++s_) {
+      kf[s_] = th2_frag(rK[e], key, a.ks[1], a.D, s_, h);
+      if (rot) kf[s_] = rope8<1>(kf[s_], a.rope, key, 16 * s_ + 8 * h);
+      vf[s_] = th2_frag(rV[e], key, a.vs[1], a.D, s_, h);
+    }
+  };
+  if constexpr (KVR) load_kv(0);
   if (w == 0) {
     Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
     mx[0 * 64 + lane] = th2_mix<false, false, KST>(a.th1, H, lane);   // T1^T, image operand
@@ -648,25 +747,22 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     mx[3 * 64 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);     // T1, accumulator operand
   }
   const Th2Mix* mx = reinterpret_cast<const Th2Mix*>(MX) + lane;
-  f32x16 adk[NT], adv[NT];
+  f32x16 adk[HPW][NT], adv[HPW][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    adk[t] = zero16();
-    adv[t] = zero16();
-  }
+  for (int e = 0; e < HPW; ++e)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      adk[e][t] = zero16();
+      adv[e][t] = zero16();
+    }
   const int nqt = (a.Nq + 31) / 32;
-  // per-wave dO / Q tiles: with <= 8 waves both images stay resident (the S / dP2 operands are read
-  // from them and the next tile is in flight during this one); 16 waves share one 4 KiB buffer
-  // per wave (dO for dV, then Q for dK) and read the S / dP2 operands from global memory
-  constexpr bool TWO = NWMAX <= 8;
-  char* bufQ = TWO ? buf + NWMAX * I::bytes(32) : buf;
   WStage<__bf16, DP, true> gst, qst;
   if constexpr (TWO) {
-    gst.load_buf(rG, 0, a.dos[1], a.D, lane);
-    qst.load_buf(rQ, 0, a.qs[1], a.D, lane);
+    gst.load_buf(rG[0], 0, a.dos[1], a.D, lane);
+    qst.load_buf(rQ[0], 0, a.qs[1], a.D, lane);
     if (rot) qst.rope(a.rope, 0, lane);
-    gst.write(buf, lane);
-    qst.write(bufQ, lane);
+    gst.write(buf[0], lane);
+    qst.write(bufQ[0], lane);
   }
   for (int qt = 0; qt < nqt; ++qt) {
     const int q = qt * 32 + r32;
@@ -674,43 +770,49 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     // BEFORE the next tile's Q / dO prefetch: waiting for them then leaves the prefetch in flight
     // (vmcnt counts in order; loaded after it, the wait drained the prefetch every tile)
     float lse2[NR], dl[NR];
+    auto load_rows = [&]() {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const size_t o = ((size_t)b * H + min(row_of(r, h), H - 1)) * a.Nq + min(q, a.Nq - 1);
-      lse2[r] = a.lse[o];
-      dl[r] = a.delta[o];
-    }
+      for (int r = 0; r < NR; ++r) {
+        const size_t o = ((size_t)b * H + min(row_of(r, h), H - 1)) * a.Nq + min(q, a.Nq - 1);
+        lse2[r] = a.lse[o];
+        dl[r] = a.delta[o];
+      }
+    };
+    if constexpr (TWO) load_rows();   // (no prefetch without TWO: loaded after the score tiles)
     if constexpr (TWO) {
       if (qt + 1 < nqt) {
-        gst.load_buf(rG, (qt + 1) * 32, a.dos[1], a.D, lane);
-        qst.load_buf(rQ, (qt + 1) * 32, a.qs[1], a.D, lane);
+        gst.load_buf(rG[0], (qt + 1) * 32, a.dos[1], a.D, lane);
+        qst.load_buf(rQ[0], (qt + 1) * 32, a.qs[1], a.D, lane);
       }
-    } else {
-      gst.load_buf(rG, qt * 32, a.dos[1], a.D, lane);
-      qst.load_buf(rQ, qt * 32, a.qs[1], a.D, lane);
     }
-    {
+#pragma unroll
+    for (int e = 0; e < HPW; ++e) {
+      if constexpr (!TWO) gst.load_buf(rG[e], qt * 32, a.dos[1], a.D, lane);
+      if constexpr (!KVR) load_kv(e);
       f32x16 s = zero16(), g = zero16();
 #pragma unroll
       for (int s_ = 0; s_ < NS; ++s_) {
         bf16x8 qa, ga;
         if constexpr (TWO) {
-          qa = I::rowfrag(bufQ, r32, s_, h);
-          ga = I::rowfrag(buf, r32, s_, h);
+          qa = I::rowfrag(bufQ[0], r32, s_, h);
+          ga = I::rowfrag(buf[0], r32, s_, h);
         } else {
-          qa = th2_frag(rQ, q, a.qs[1], a.D, s_, h);
+          qa = th2_frag(rQ[e], q, a.qs[1], a.D, s_, h);
           if (rot) qa = rope8<1>(qa, a.rope, q, 16 * s_ + 8 * h);
-          ga = th2_frag(rG, q, a.dos[1], a.D, s_, h);
+          ga = th2_frag(rG[e], q, a.dos[1], a.D, s_, h);
         }
         if (s_ < NS - 1 || full) {   // query rows, key lanes (th2_put)
           s = MF<__bf16>::mma(qa, kf[s_], s);
           g = MF<__bf16>::mma(ga, vf[s_], g);
         }
       }
-      th2_put(XS, w, s, a.scale, lane);
-      th2_put(XG, w, g, 1.f, lane);
+      if (hv[e]) {
+        th2_put(XS, hd[e], s, a.scale, lane);
+        th2_put(XG, hd[e], g, 1.f, lane);
+      }
+      if constexpr (!TWO) gst.write(buf[e], lane);
     }
-    if constexpr (!TWO) gst.write(buf, lane);
+    if constexpr (!TWO) load_rows();
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -718,17 +820,17 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
       lse2[r] = ok ? lse2[r] * kLog2e : kInf;
       dl[r] = ok ? dl[r] : 0.f;
     }
-    constexpr int G = 2;   // blocks (keys) per group: independent chains issued together
-    for (int b0 = w; b0 < 32; b0 += G * H) {
+    constexpr int G = HPW == 1 ? 2 : 1;   // blocks (keys) per group: independent chains issued together
+    for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 p[G], dp[G];
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        p[u] = th2_mix_img<KST>(XS, (b0 + u * H) & 31, mx[0], lane);
-        dp[u] = th2_mix_img<KST>(XG, (b0 + u * H) & 31, mx[2 * 64], lane);
+        p[u] = th2_mix_img<KST>(XS, (b0 + u * NW) & 31, mx[0], lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * NW) & 31, mx[2 * 64], lane);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        const int blk = b0 + u * H;   // blk = key of this block
+        const int blk = b0 + u * NW;   // blk = key of this block
         const bool ok = kb * 32 + blk < a.Nk;   // keys past the end: P2 = dS = 0
         f32x16 ds1;
 #pragma unroll
@@ -751,52 +853,65 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = th2_rowB(XS, w, s2, lane);
+    for (int e = 0; e < HPW; ++e) {
+      const int he = hv[e] ? hd[e] : w;
+      if constexpr (!TWO) qst.load_buf(rQ[e], qt * 32, a.qs[1], a.D, lane);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) adv[t] = MF<__bf16>::mma(I::colfrag(buf, 0, s2, 32 * t, lane), pf, adv[t]);
-    }
-    if constexpr (!TWO) {   // one buffer: Q after this wave's own dO reads
-      if (rot) qst.rope(a.rope, qt * 32, lane);
-      qst.write(bufQ, lane);
-    }
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = th2_rowB(XS, he, s2, lane);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 sf = th2_rowB(XG, w, s2, lane);
+        for (int t = 0; t < NT; ++t)
+          adv[e][t] = MF<__bf16>::mma(I::colfrag(buf[e], 0, s2, 32 * t, lane), pf, adv[e][t]);
+      }
+      if constexpr (!TWO) {   // one buffer: Q after this wave's own dO reads
+        if (rot) qst.rope(a.rope, qt * 32, lane);
+        qst.write(bufQ[e], lane);
+      }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) adk[t] = MF<__bf16>::mma(I::colfrag(bufQ, 0, s2, 32 * t, lane), sf, adk[t]);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 sf = th2_rowB(XG, he, s2, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          adk[e][t] = MF<__bf16>::mma(I::colfrag(bufQ[e], 0, s2, 32 * t, lane), sf, adk[e][t]);
+      }
     }
     if constexpr (TWO) {
       if (qt + 1 < nqt) {   // wave-private images: after this wave's own reads
         if (rot) qst.rope(a.rope, (qt + 1) * 32, lane);
-        gst.write(buf, lane);
-        qst.write(bufQ, lane);
+        gst.write(buf[0], lane);
+        qst.write(bufQ[0], lane);
       }
     }
     __syncthreads();
   }
   if (key < a.Nk) {
-    __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + w * a.dks[2] + (long long)key * a.dks[1];
-    __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + w * a.dvs[2] + (long long)key * a.dvs[1];
     const float sc = a.scale;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int e = 0; e < HPW; ++e) {
+      if (!hv[e]) continue;
+      __bf16* DK = reinterpret_cast<__bf16*>(a.dk) + b * a.dks[0] + hd[e] * a.dks[2] + (long long)key * a.dks[1];
+      __bf16* DV = reinterpret_cast<__bf16*>(a.dv) + b * a.dvs[0] + hd[e] * a.dvs[2] + (long long)key * a.dvs[1];
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * t + 8 * g4 + 4 * h;
-        float x[4];
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[e] = (float)(__bf16)(adk[t][4 * g4 + e] * sc);
-        if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, key, d0 / 2);
-        store4<__bf16, true>(DK, d0, a.D, x[0], x[1], x[2], x[3]);
-        store4<__bf16, true>(DV, d0, a.D, adv[t][4 * g4], adv[t][4 * g4 + 1], adv[t][4 * g4 + 2], adv[t][4 * g4 + 3]);
-      }
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * t + 8 * g4 + 4 * h;
+          float x[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[c] = (float)(__bf16)(adk[e][t][4 * g4 + c] * sc);
+          if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, key, d0 / 2);
+          store4<__bf16, true>(DK, d0, a.D, x[0], x[1], x[2], x[3]);
+          store4<__bf16, true>(DV, d0, a.D, adv[e][t][4 * g4], adv[e][t][4 * g4 + 1], adv[e][t][4 * g4 + 2],
+                               adv[e][t][4 * g4 + 3]);
+        }
+    }
   }
 }
 
-// LDS: two exchange images + per-wave 32-row staging (two per wave in th2_bwd_kv at <= 8 waves)
-template <int DP, bool KST> constexpr size_t th2_lds_bytes(int H) {
-  return 2 * (size_t)th2_img<KST>() + (size_t)H * Img<__bf16, DP>::bytes(32);
+// LDS: two exchange images + per-head 32-row staging (two per head in th2_bwd_kv at <= 8 waves);
+// th2_bwd_q with two heads per wave adds its mix-operand table (3 x 64 lanes x 32 bytes)
+template <int DP, bool KST> constexpr size_t th2_lds_bytes(int H, int hpw = 1) {
+  return 2 * (size_t)th2_img<KST>() + (size_t)H * Img<__bf16, DP>::bytes(32) + (hpw > 1 ? 3 * 64 * 32 : 0);
 }
 
 template <int DP, bool KST> constexpr size_t th2_kv_lds_bytes(int H, bool two_buffers) {

@@ -34,6 +34,8 @@ def _orth(rng, h):
     (2, 196, 196, 16, 48, "bf16"),   # cait_m_24 / _36 / _48: 16 heads (create_model.py:142-168)
     (1, 70, 45, 12, 48, "bf16"),     # 12 heads, ragged, Nq != Nk
     (2, 50, 50, 4, 48, "bf16"),      # cait_xxs heads
+    (1, 45, 45, 9, 48, "bf16"),      # odd head count > 8: the last wave's second head is empty
+    (1, 40, 33, 11, 32, "bf16"),     # 11 heads at head_dim 32, Nq != Nk
 ])
 def test_talking_heads(dev, B, N, Nk, H, D, mode):
     import torch
