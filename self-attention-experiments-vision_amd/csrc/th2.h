@@ -771,11 +771,26 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
     // (vmcnt counts in order; loaded after it, the wait drained the prefetch every tile)
     float lse2[NR], dl[NR];
     auto load_rows = [&]() {
+      if constexpr (HPW == 1) {   // rows past H clamped (masked after the barrier)
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const size_t o = ((size_t)b * H + min(row_of(r, h), H - 1)) * a.Nq + min(q, a.Nq - 1);
-        lse2[r] = a.lse[o];
-        dl[r] = a.delta[o];
+        for (int r = 0; r < NR; ++r) {
+          const size_t o = ((size_t)b * H + min(row_of(r, h), H - 1)) * a.Nq + min(q, a.Nq - 1);
+          lse2[r] = a.lse[o];
+          dl[r] = a.delta[o];
+        }
+      } else {
+        // one per-lane base (head 4h, query q) plus wave-uniform row offsets: the 64-bit offsets
+        // per register above, hoisted out of the loop, were what spilled at two heads per wave
+        const size_t base = ((size_t)b * H + 4 * h) * a.Nq + min(q, a.Nq - 1);
+        const float* lrow = a.lse + base;
+        const float* drow = a.delta + base;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int off = ((r & 3) + 8 * (r >> 2)) * a.Nq;   // (row_of(r, h) - 4h) Nq
+          const bool in = row_of(r, h) < H;
+          lse2[r] = in ? lrow[off] : 0.f;
+          dl[r] = in ? drow[off] : 0.f;
+        }
       }
     };
     if constexpr (TWO) load_rows();   // (no prefetch without TWO: loaded after the score tiles)
@@ -832,22 +847,21 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;   // blk = key of this block
         const bool ok = kb * 32 + blk < a.Nk;   // keys past the end: P2 = dS = 0
-        f32x16 ds1;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
+        for (int r = 0; r < NR; ++r) {   // dp[u] becomes dS1 in place
           p[u][r] = ok ? ex2(__builtin_fmaf(p[u][r], kLog2e, -lse2[r])) : 0.f;
-          ds1[r] = p[u][r] * (dp[u][r] - dl[r]);
+          dp[u][r] = p[u][r] * (dp[u][r] - dl[r]);
         }
         if constexpr (!KST) {
 #pragma unroll
           for (int r = 8; r < 16; ++r) {
             p[u][r] = 0.f;
-            ds1[r] = 0.f;
+            dp[u][r] = 0.f;
           }
         }
         if (blk < 32) {
-          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(p[u], mx[64]), H, lane);     // P2_h over S_h at this key
-          th2_put_block<NR>(XG, blk, th2_mix_acc<KST>(ds1, mx[3 * 64]), H, lane);  // dS_h over dP2_h
+          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(p[u], mx[64]), H, lane);       // P2_h over S_h at this key
+          th2_put_block<NR>(XG, blk, th2_mix_acc<KST>(dp[u], mx[3 * 64]), H, lane);  // dS_h over dP2_h
         }
       }
     }
