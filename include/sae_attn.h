@@ -194,12 +194,19 @@ int sae_gemm_dw_blocked(void* stream, int32_t M, int32_t I, int32_t J, int32_t j
      SAE_EPI_NONE : c = bf16(acc + bias)
      SAE_EPI_GELU : c2 = h = bf16(acc + bias), c = bf16(gelu(h))
      SAE_EPI_DGELU: c = bf16(bf16(acc) * gelu'(aux))   (aux bf16 [M][N], ldaux; bias NULL)
+     SAE_EPI_GELU_GRAD: c2 = g = bf16(gelu'(bf16(acc + bias))), c = bf16(gelu(bf16(acc + bias)))
+     SAE_EPI_MUL_AUX  : c = bf16(bf16(acc) * aux)       (aux = the g above; bias NULL)
+   (the FF block's pair: the forward saves gelu'(h) instead of h, so the input-gradient GEMM's
+   epilogue is one multiply instead of the sigmoid algebra -- gelu' rounded to bf16 once, the
+   rounding the reference's bf16 derivative carries anyway)
    c, c2 bf16 [M][N] (ldc); bias fp32 [N] or NULL.  K a multiple of 8; N, lda, ldb, ldc
    multiples of 8; pointers 16-byte aligned.  A Dense forward passes the transposed bf16
    kernel as bt (see sae_weight_cast); its input gradient passes the kernel itself. */
 #define SAE_EPI_NONE 0
 #define SAE_EPI_GELU 1
 #define SAE_EPI_DGELU 2
+#define SAE_EPI_GELU_GRAD 3
+#define SAE_EPI_MUL_AUX 4
 int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, int64_t lda,
                 const void* bt, int64_t ldb, const float* bias, void* c, int64_t ldc,
                 int32_t epilogue, const void* aux, int64_t ldaux, void* c2);

@@ -466,7 +466,7 @@ template <int DP, int NWMAX, bool ROT, int HPW> int th2_bwd_run(hipStream_t st, 
   constexpr bool KST = NWMAX * HPW <= 8;
   const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32, nw = (a.H + HPW - 1) / HPW;
   a.nblk = nqb * a.B;
-  const size_t lds = th2_lds_bytes<DP, KST>(a.H, HPW), lds_kv = th2_kv_lds_bytes<DP, KST>(a.H, KST);
+  const size_t lds = th2_lds_bytes<DP, KST>(a.H, HPW), lds_kv = th2_kv_lds_bytes<DP, KST>(a.H, KST && HPW == 1);
   if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>, lds)) return rc;
   if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT, HPW>, lds_kv)) return rc;
   hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
@@ -1296,8 +1296,9 @@ int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, 
 
 // ------------------------------------------------------------ forward / input-gradient GEMMs
 int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
-  if (M < 1 || N < 1 || K < 1 || K % 8 || N % 8 || epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_DGELU)
+  if (M < 1 || N < 1 || K < 1 || K % 8 || N % 8 || epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_MUL_AUX)
     return SAE_NT_ROUTE_NONE;
+  if (epilogue >= SAE_EPI_GELU_GRAD) epilogue -= 2;   // the gelu' forms run on the GELU / GELU' kernels
   if (g8x_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8X;
   if (g8_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8;
   return K % kNtK ? SAE_NT_ROUTE_TILE128_KTAIL : SAE_NT_ROUTE_TILE128;
@@ -1312,8 +1313,11 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
     return fail(SAE_EINVAL, "gemm_nt: bad leading dimensions lda %lld ldb %lld ldc %lld", (long long)lda,
                 (long long)ldb, (long long)ldc);
   if (!a || !bt || !c) return fail(SAE_EINVAL, "gemm_nt: a/bt/c must be non-NULL");
-  if (epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_DGELU)
+  if (epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_MUL_AUX)
     return fail(SAE_EINVAL, "gemm_nt: unknown epilogue %d", epilogue);
+  // SAE_EPI_GELU_GRAD / SAE_EPI_MUL_AUX: the GELU / GELU' kernels with the saved operand gelu'(h)
+  const bool gp = epilogue >= SAE_EPI_GELU_GRAD;
+  if (gp) epilogue -= 2;
   if (epilogue == SAE_EPI_GELU && !c2) return fail(SAE_EINVAL, "gemm_nt: the GELU epilogue needs c2 (pre-activation out)");
   if (epilogue == SAE_EPI_DGELU && (!aux || ldaux < N || ldaux % 8 || bias))
     return fail(SAE_EINVAL, "gemm_nt: the GELU-derivative epilogue needs aux (ldaux >= N, multiple of 8) and no bias");
@@ -1327,6 +1331,7 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   g.bt = reinterpret_cast<const __bf16*>(bt);
   g.bias = bias;
   g.aux = reinterpret_cast<const __bf16*>(aux);
+  g.gp = gp ? 1 : 0;
   g.c = reinterpret_cast<__bf16*>(c);
   g.c2 = reinterpret_cast<__bf16*>(c2);
   g.M = M;

@@ -293,14 +293,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
           if constexpr (EPI == kEpiNone) {
             *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
           } else if constexpr (EPI == kEpiGelu) {
-            *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
-            const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
-            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+            gelu_store8(raw, a.gp, a.c + (long long)m * a.ldc + n, a.c2 + (long long)m * a.ldc + n);
           } else {
-            const uint4 h = hv[ip][it];
-            const uint4 y = {dgelu_bf2(raw.x, h.x), dgelu_bf2(raw.y, h.y), dgelu_bf2(raw.z, h.z),
-                             dgelu_bf2(raw.w, h.w)};
-            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = dgelu8(raw, hv[ip][it], a.gp);
           }
         }
       }
@@ -477,9 +472,7 @@ __global__ __launch_bounds__(512, 1) void gemm8x_nt_kernel(NtArgs a) {
       if constexpr (EPI == kEpiNone) {
         *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
       } else {
-        *reinterpret_cast<uint4*>(a.c2 + (long long)m * a.ldc + n) = raw;
-        const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
-        *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = y;
+        gelu_store8(raw, a.gp, a.c + (long long)m * a.ldc + n, a.c2 + (long long)m * a.ldc + n);
       }
     }
   }

@@ -10,6 +10,10 @@
 //   kEpiNone : c = bf16(acc + bias)
 //   kEpiGelu : c2 = h = bf16(acc + bias) (saved for the backward), c = bf16(gelu(h))
 //   kEpiDGelu: c = bf16(bf16(acc) * gelu'(aux))   (aux = the saved h; the FF block's dH)
+// with NtArgs::gp set (the C ABI's SAE_EPI_GELU_GRAD / SAE_EPI_MUL_AUX, the FF block's pair) the
+// forward saves g = bf16(gelu'(h)) instead of h (same sigmoid, a few more packed FMAs) and the
+// backward epilogue is one multiply, c = bf16(bf16(acc) * g): the sigmoid / rcp work of GELU'
+// leaves the input-gradient GEMM, whose epilogue bounded it.
 // which removes the two elementwise HBM passes (GELU forward, GELU backward) per FF block.
 //
 // Structure (gfx950): a 128 x 128 output tile per 256-thread workgroup, 4 waves of 64 x 64 (2 x 2
@@ -39,6 +43,7 @@ struct NtArgs {
   int M, N, K;
   long long lda, ldb, ldc, ldaux;
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
+  int gp;              // kEpiGelu: c2 = gelu'(h) instead of h; kEpiDGelu: aux holds gelu'(h)
 };
 
 constexpr int kNtT = 128;   // output tile edge
@@ -87,6 +92,37 @@ __device__ __forceinline__ unsigned dgelu_bf2(unsigned dw, unsigned hw) {   // d
   const f32x2 q = s - s * s;                                    // s (1 - s)
   const f32x2 poly = (2.f * kGeluB) + (6.f * kGeluB * kGeluK) * (x * x);
   return f2_to_bf2(bf2_to_f2(dw) * ((x * q) * poly + s));
+}
+// gelu(h) and gelu'(h) of a bf16 pair from one sigmoid (the gp forward epilogue)
+__device__ __forceinline__ unsigned gelu_grad_bf2(unsigned hw, unsigned& gw) {
+  const f32x2 x = bf2_to_f2(hw);
+  const f32x2 s = gelu_sig2(x);
+  const f32x2 q = s - s * s;
+  const f32x2 poly = (2.f * kGeluB) + (6.f * kGeluB * kGeluK) * (x * x);
+  gw = f2_to_bf2((x * q) * poly + s);
+  return f2_to_bf2(x * s);
+}
+__device__ __forceinline__ unsigned mul_bf2(unsigned dw, unsigned gw) {   // d * g (the gp backward epilogue)
+  return f2_to_bf2(bf2_to_f2(dw) * bf2_to_f2(gw));
+}
+// the GELU / GELU' epilogue stores of one 16-byte row segment (8 outputs)
+__device__ __forceinline__ void gelu_store8(const uint4& raw, bool gp, __bf16* c, __bf16* c2) {
+  if (gp) {
+    uint4 g, y;
+    y.x = gelu_grad_bf2(raw.x, g.x);
+    y.y = gelu_grad_bf2(raw.y, g.y);
+    y.z = gelu_grad_bf2(raw.z, g.z);
+    y.w = gelu_grad_bf2(raw.w, g.w);
+    *reinterpret_cast<uint4*>(c2) = g;
+    *reinterpret_cast<uint4*>(c) = y;
+  } else {
+    *reinterpret_cast<uint4*>(c2) = raw;
+    *reinterpret_cast<uint4*>(c) = uint4{gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
+  }
+}
+__device__ __forceinline__ uint4 dgelu8(const uint4& raw, const uint4& hv, bool gp) {
+  if (gp) return uint4{mul_bf2(raw.x, hv.x), mul_bf2(raw.y, hv.y), mul_bf2(raw.z, hv.z), mul_bf2(raw.w, hv.w)};
+  return uint4{dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z), dgelu_bf2(raw.w, hv.w)};
 }
 
 // one operand's ROWS x BK stage: ROWS * BK / 8 16-byte chunks, ROWS * BK / 2048 per thread.
@@ -430,14 +466,9 @@ __global__ __launch_bounds__(256, (nt_min_blocks<EPI, AL>())) void gemm_nt_kerne
         if constexpr (EPI == kEpiNone) {
           *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = raw;
         } else if constexpr (EPI == kEpiGelu) {
-          *reinterpret_cast<uint4*>(a.c2 + orow * a.ldc + n) = raw;
-          const uint4 y = {gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
-          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;
+          gelu_store8(raw, a.gp, a.c + orow * a.ldc + n, a.c2 + orow * a.ldc + n);
         } else {
-          const uint4 hv = auxv[UM == 2 ? u : 0][it];
-          const uint4 y = {dgelu_bf2(raw.x, hv.x), dgelu_bf2(raw.y, hv.y), dgelu_bf2(raw.z, hv.z),
-                           dgelu_bf2(raw.w, hv.w)};
-          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = y;
+          *reinterpret_cast<uint4*>(a.c + orow * a.ldc + n) = dgelu8(raw, auxv[UM == 2 ? u : 0][it], a.gp);
         }
       }
     }

@@ -707,7 +707,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   // per-wave dO / Q tiles: with <= 8 heads both images stay resident (the S / dP2 operands are read
   // from them and the next tile is in flight during this one); otherwise one 4 KiB buffer per head
   // (dO for dV, then Q for dK) and the S / dP2 operands come from global memory
-  constexpr bool TWO = NWMAX * HPW <= 8;
+  constexpr bool TWO = NWMAX * HPW <= 8 && HPW == 1;
   int hd[HPW];
   bool hv[HPW];
   char *buf[HPW], *bufQ[HPW];

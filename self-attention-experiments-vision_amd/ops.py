@@ -19,6 +19,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -1042,6 +1043,10 @@ def patch_embed_ok(images: torch.Tensor, w: torch.Tensor, patch: Tuple[int, int]
 
 # ------------------------------------------------- forward / input-gradient GEMMs (sae_gemm_nt)
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
+# the FF block's pair (include/sae_attn.h): the forward saves g = gelu'(h) instead of h, the
+# input-gradient epilogue multiplies by it
+EPI_GELU_GRAD, EPI_MUL_AUX = 3, 4
+FF_GELU_GRAD = os.environ.get("SAE_FF_GELU_GRAD", "1") != "0"   # (False: save h, GELU' epilogue; A/B)
 
 
 # Every bf16 forward / input-gradient projection whose widths are multiples of 8 runs on
@@ -1080,7 +1085,8 @@ def weight_cast(w: torch.Tensor, plain: bool = True, transposed: bool = True):
 def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
             aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
     """``epi(a2 @ bt^T (+ bias))`` through ``sae_gemm_nt``: a2 [M, K], bt [N, K] bf16.  Returns c,
-    or (c, h) for the GELU epilogue (c = gelu(h), h = the bf16 pre-activation)."""
+    or (c, h) for the GELU epilogue (c = gelu(h), h = the bf16 pre-activation), or (c, g) for
+    EPI_GELU_GRAD (g = bf16(gelu'(h)), the aux of a later EPI_MUL_AUX call)."""
     lib = L.load()
     _require_gpu(a2, bt)
     M, K = a2.shape
@@ -1096,9 +1102,9 @@ def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = N
     else:
         c = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
     # the kernel writes c2 with c's row stride (ldc): give it the same layout
-    c2 = torch.empty_strided((M, N), (c.stride(0), 1), dtype=torch.bfloat16, device=a2.device) \
-        if epilogue == EPI_GELU else None
-    if epilogue == EPI_DGELU:
+    two = epilogue in (EPI_GELU, EPI_GELU_GRAD)
+    c2 = torch.empty_strided((M, N), (c.stride(0), 1), dtype=torch.bfloat16, device=a2.device) if two else None
+    if epilogue in (EPI_DGELU, EPI_MUL_AUX):
         if aux is None or aux.dtype != torch.bfloat16 or tuple(aux.shape) != (M, N):
             raise ValueError(f"gemm_nt: the GELU-derivative epilogue needs a bf16 aux [{M}, {N}]")
     if aux is not None and aux.stride(1) != 1:
@@ -1108,13 +1114,14 @@ def gemm_nt(a2: torch.Tensor, bt: torch.Tensor, bias: Optional[torch.Tensor] = N
     L.check(lib.sae_gemm_nt(_stream(a2), M, N, K, _ptr(a2), a2.stride(0), _ptr(bt), bt.stride(0), _ptr(bias),
                             _ptr(c), c.stride(0), int(epilogue), _ptr(aux), aux.stride(0) if aux is not None else 0,
                             _ptr(c2)))
-    return (c, c2) if epilogue == EPI_GELU else c
+    return (c, c2) if two else c
 
 
 class _FFBlock(torch.autograd.Function):
     """ff.py:8-34 in bf16: ``Dense_1(gelu(Dense_0(x)))`` with the GELU fused into Dense_0's GEMM
-    epilogue (saving the pre-activation h) and its derivative fused into the epilogue of Dense_1's
-    input-gradient GEMM; weight / bias gradients through ``sae_gemm_dw``."""
+    epilogue (saving gelu'(h) of the pre-activation h, EPI_GELU_GRAD) and the product with it fused
+    into the epilogue of Dense_1's input-gradient GEMM (EPI_MUL_AUX); weight / bias gradients
+    through ``sae_gemm_dw``."""
 
     @staticmethod
     def forward(ctx, x, w0, b0, w1, b1):
@@ -1124,9 +1131,11 @@ class _FFBlock(torch.autograd.Function):
             x2 = x2.contiguous()
         w0p, w0t = _cast([w0], torch.bfloat16)
         w1p, w1t = _cast([w1], torch.bfloat16)
-        a, h = gemm_nt(x2, w0t, b0, EPI_GELU)
+        gg = FF_GELU_GRAD
+        a, h = gemm_nt(x2, w0t, b0, EPI_GELU_GRAD if gg else EPI_GELU)   # h: gelu'(pre-activation)
         y = gemm_nt(a, w1t, b1)                                   # Dense_1 forward
         ctx.save_for_backward(x2, h, a, w0p, w1p)
+        ctx.gg = gg
         ctx.xshape, ctx.xdtype, ctx.has_b = x.shape, x.dtype, (b0 is not None, b1 is not None)
         ctx.sinks = [_sink(t) for t in (w0, b0, w1, b1)]
         return y.view(*x.shape[:-1], w1.shape[1])
@@ -1140,7 +1149,7 @@ class _FFBlock(torch.autograd.Function):
         dy2 = dy.to(torch.bfloat16).reshape(-1, O)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8 or dy2.data_ptr() % 16:
             dy2 = dy2.contiguous()
-        dh = gemm_nt(dy2, w1p, None, EPI_DGELU, aux=h)            # dA W1^T, times gelu'(h)
+        dh = gemm_nt(dy2, w1p, None, EPI_MUL_AUX if ctx.gg else EPI_DGELU, aux=h)   # dA W1^T, times gelu'(h)
         sw0, sb0, sw1, sb1 = ctx.sinks   # flat-buffer sinks (multi-rank step): written in place
         dev = dy2.device
         dw1 = _claim(sw1) if sw1 is not None else torch.empty((Hd, O), dtype=torch.float32, device=dev)

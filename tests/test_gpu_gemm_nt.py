@@ -317,3 +317,30 @@ def test_gemm_nt_ktail_rowstride(dev):
     bt = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
     c = ops.gemm_nt(a, bt)
     assert _rel(c, a.double() @ bt.double().t()) <= 1e-2
+
+
+@pytest.mark.parametrize("M,K,N", [(25216, 384, 1536), (197, 768, 1000), (6000, 768, 3072), (300, 368, 1472)])
+def test_gemm_nt_gelu_grad_pair(dev, M, K, N):
+    """The FF block's epilogue pair: EPI_GELU_GRAD returns gelu(h) bit-equal to EPI_GELU's and
+    g = bf16(gelu'(h)) of the same bf16 pre-activation; EPI_MUL_AUX multiplies bf16(acc) by g."""
+    import sae_vision_amd.ops as ops
+    from sae_vision_amd import _lib as L
+    lib = L.load()
+    for epi, plain in ((ops.EPI_GELU_GRAD, ops.EPI_GELU), (ops.EPI_MUL_AUX, ops.EPI_DGELU)):
+        assert lib.sae_gemm_nt_route(M, N, K, epi) == lib.sae_gemm_nt_route(M, N, K, plain)
+    a, bt, b = _inputs(dev, M, K, N, 21)
+    y, g = ops.gemm_nt(a, bt, b, ops.EPI_GELU_GRAD)
+    y_ref, h = ops.gemm_nt(a, bt, b, ops.EPI_GELU)
+    assert torch.equal(y, y_ref)
+    hf = h.float().requires_grad_(True)
+    F.gelu(hf, approximate="tanh").sum().backward()
+    gref = hf.grad
+    assert float((g.float() - gref).abs().max()) <= 2 ** -8 * float(gref.abs().max()) + 1e-6
+    # the input-gradient side: dY [M, N'] x W [N', N] -> dA [M, N] times g
+    a2, bt2, _ = _inputs(dev, M, N, N, 22)
+    dh = ops.gemm_nt(a2, bt2, None, ops.EPI_MUL_AUX, aux=g)
+    da = (a2.double() @ bt2.double().t()).to(torch.bfloat16).float()
+    assert _rel(dh, da * g.float()) <= 1e-2
+    # and against the GELU' epilogue from h: the one extra bf16 rounding of gelu'
+    dh_ref = ops.gemm_nt(a2, bt2, None, ops.EPI_DGELU, aux=h)
+    assert _rel(dh, dh_ref.float()) <= 2e-2
