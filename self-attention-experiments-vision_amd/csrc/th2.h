@@ -63,15 +63,16 @@ __device__ __forceinline__ bf16x8 th2_tr2(const char* p1, const char* p2) {
 struct Th2Mix {
   bf16x8 hi, lo;
 };
+// `mul` scales T before the split (th2_fwd: log2 e, so the mixed logits come out in the log2 domain)
 template <bool TR, bool PERM, bool KST>
-__device__ __forceinline__ Th2Mix th2_mix(const float* T, int H, int lane) {
+__device__ __forceinline__ Th2Mix th2_mix(const float* T, int H, int lane, float mul = 1.f) {
   Th2Mix m;
   const int row = lane & 31, g = lane >> 5;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = PERM ? 8 * (j >> 2) + 4 * g + (j & 3) : 8 * g + j;
     const int hd = KST ? (k & 7) : k;
-    const float t = (row < H && hd < H) ? (TR ? T[row * H + hd] : T[hd * H + row]) : 0.f;
+    const float t = (row < H && hd < H) ? (TR ? T[row * H + hd] : T[hd * H + row]) * mul : 0.f;
     const __bf16 hi = (__bf16)t;
     const __bf16 lo = (__bf16)(t - (float)hi);
     if constexpr (KST) {
@@ -97,17 +98,25 @@ __device__ __forceinline__ f32x16 th2_mix_img(const char* img, int blk, const Th
   return MF<__bf16>::mma(m.lo, b, c);
 }
 
+// two fp32 values -> one dword of two bf16 (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned th2_pk(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f2v;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2v;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{a, b}, b2v));
+}
+
 // mixed tile from an accumulator (rows = heads < 16, lanes = positions); KST: registers 4..7
-// (rows 8..15) take a copy of 0..3 (rows 0..7), the second K half of the stacked operand
+// (rows 8..15) take a copy of 0..3 (rows 0..7), the second K half of the stacked operand.  The
+// operand is packed pairwise (element-wise conversion left single-value conversions plus v_perm
+// re-packing in the hot loops)
 template <bool KST>
 __device__ __forceinline__ f32x16 th2_mix_acc(const f32x16& x, const Th2Mix& m) {
   if constexpr (KST) {
-    f32x16 y = x;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y[4 + r] = x[r];
-    return MF<__bf16>::mma(m.hi, acc_frag<__bf16>(y, 0), zero16());
+    const unsigned p0 = th2_pk(x[0], x[1]), p1 = th2_pk(x[2], x[3]);
+    return MF<__bf16>::mma(m.hi, __builtin_bit_cast(bf16x8, uint4{p0, p1, p0, p1}), zero16());
   } else {
-    const bf16x8 b = acc_frag<__bf16>(x, 0);
+    const bf16x8 b = __builtin_bit_cast(
+        bf16x8, uint4{th2_pk(x[0], x[1]), th2_pk(x[2], x[3]), th2_pk(x[4], x[5]), th2_pk(x[6], x[7])});
     f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
     return MF<__bf16>::mma(m.lo, b, c);
   }
@@ -131,6 +140,11 @@ template <int NR>
 __device__ __forceinline__ void th2_put_block(char* img, int blk, const f32x16& v, int H, int lane) {
   char* p = img + blk * kTh2Blk + (lane & 31) * 2;
   const int h = lane >> 5;
+  if (H >= 2 * NR) {   // every row of the registers is a head (wave-uniform): no per-lane branches
+#pragma unroll
+    for (int r = 0; r < NR; ++r) *reinterpret_cast<__bf16*>(p + row_of(r, h) * kTh2Row) = (__bf16)v[r];
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int i = row_of(r, h);
@@ -258,7 +272,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       qf[e][s] = th2_frag(rQ[e], q, a.qs[1], a.D, s, h);
       if (rot) qf[e][s] = rope8<1>(qf[e][s], a.rope, q, 16 * s + 8 * h);
     }
-  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane);   // S1 = T1^T S
+  // S1 = T1^T S with T1 scaled by log2 e: the mixed logits come out in the log2 domain, so the
+  // statistics and probabilities need no per-element scaling
+  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);
   const Th2Mix m2 = th2_mix<false, true, KST>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
   const int nkt = (a.Nk + 31) / 32;
 
@@ -313,11 +329,11 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (ok[u]) mx = fmaxf(mx, c[u][r]);
-        const float mn = fmaxf(m[r], mx * kLog2e);
+        const float mn = fmaxf(m[r], mx);
         float sum = l[r] * ex2(m[r] - mn);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (ok[u]) sum += ex2(__builtin_fmaf(c[u][r], kLog2e, -mn));
+          if (ok[u]) sum += ex2(c[u][r] - mn);
         l[r] = sum;
         m[r] = mn;
       }
@@ -345,10 +361,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
         ll = (mm == -kInf ? 0.f : ll * ex2(mm - mn)) + (v.x == -kInf ? 0.f : v.y * ex2(v.x - mn));
         mm = mn;
       }
-      m[r] = mm;
-      l[r] = 1.f / ll;   // from here on: 1 / row sum
+      m[r] = mm + lg2(ll);   // from here on: log2 of the row's normaliser, P = 2^(S1 - m)
       const int i = row_of(r, h);
-      if (w == 0 && i < H && q < a.Nq) a.lse[((size_t)b * H + i) * a.Nq + q] = (mm + lg2(ll)) * kLn2;
+      if (w == 0 && i < H && q < a.Nq) a.lse[((size_t)b * H + i) * a.Nq + q] = m[r] * kLn2;
     }
     __syncthreads();
     th2_zero_pad<KST>(XS, H, tid, 64 * NW);   // the scratch overwrote the pad rows
@@ -365,6 +380,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
     const char* xs = XS;
     char* xp = XP;
     constexpr int G = KST ? 4 : 2;   // blocks per group: independent chains issued together
+    const bool whole = kt * 32 + 32 <= a.Nk;   // every key of the tile exists (wave-uniform)
     for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 c[G];
 #pragma unroll
@@ -372,9 +388,13 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;
-        const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: P = 0
+        if (whole || kt * 32 + blk < a.Nk) {
 #pragma unroll
-        for (int r = 0; r < NR; ++r) c[u][r] = ok ? ex2(__builtin_fmaf(c[u][r], kLog2e, -m[r])) * l[r] : 0.f;
+          for (int r = 0; r < NR; ++r) c[u][r] = ex2(c[u][r] - m[r]);
+        } else {   // keys past the end: P = 0
+#pragma unroll
+          for (int r = 0; r < NR; ++r) c[u][r] = 0.f;
+        }
         if constexpr (!KST) {
 #pragma unroll
           for (int r = 8; r < 16; ++r) c[u][r] = 0.f;
@@ -488,11 +508,11 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   Th2Mix m1r, m2tr, m1tr;
   Th2Mix* const mxt = reinterpret_cast<Th2Mix*>(smem + 2 * IMG + H * I::bytes(32));
   if constexpr (HPW == 1) {
-    m1r = th2_mix<false, false, KST>(a.th1, H, lane);    // S1 = T1^T S        (image)
+    m1r = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);   // S1 = T1^T S, log2 domain (image)
     m2tr = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
     m1tr = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
   } else if (w == 0) {
-    mxt[lane] = th2_mix<false, false, KST>(a.th1, H, lane);
+    mxt[lane] = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);
     mxt[64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);
     mxt[128 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);
   }
@@ -570,13 +590,13 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;
-        const bool ok = blk < 32 && kt * 32 + blk < a.Nk;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          p[u][r] = ex2(__builtin_fmaf(p[u][r], kLog2e, -lse2[r]));
-          dl[r] += ok ? p[u][r] * dp[u][r] : 0.f;
-        }
+        const bool ok = blk < 32 && kt * 32 + blk < a.Nk;   // (wave-uniform)
         if (ok) {
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            p[u][r] = ex2(p[u][r] - lse2[r]);   // (S1 in the log2 domain: T1 carries log2 e)
+            dl[r] += p[u][r] * dp[u][r];
+          }
           th2_put_block<NR>(XS, blk, p[u], H, lane);   // P over S at this block (only this wave touches it)
           dt2 = th2_dt<KST>(XS, XG, blk, dt2, lane);   // dT2[h][i] += sum P_h dP2_i
         }
@@ -626,10 +646,14 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;
-        const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: dS = 0
+        const bool ok = kt * 32 + blk < a.Nk;   // keys past the end: dS = 0 (wave-uniform)
+        if (ok) {
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
-          ds1[u][r] = ok ? ex2(__builtin_fmaf(ds1[u][r], kLog2e, -lse2[r])) * (dp[u][r] - dl[r]) : 0.f;
+          for (int r = 0; r < NR; ++r) ds1[u][r] = ex2(ds1[u][r] - lse2[r]) * (dp[u][r] - dl[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < NR; ++r) ds1[u][r] = 0.f;
+        }
         if constexpr (!KST) {
 #pragma unroll
           for (int r = 8; r < 16; ++r) ds1[u][r] = 0.f;
@@ -741,7 +765,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   if constexpr (KVR) load_kv(0);
   if (w == 0) {
     Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
-    mx[0 * 64 + lane] = th2_mix<false, false, KST>(a.th1, H, lane);   // T1^T, image operand
+    mx[0 * 64 + lane] = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);   // log2 e T1^T, image operand
     mx[1 * 64 + lane] = th2_mix<false, true, KST>(a.th2, H, lane);    // T2^T, accumulator operand
     mx[2 * 64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);    // T2, image operand
     mx[3 * 64 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);     // T1, accumulator operand
@@ -846,11 +870,16 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;   // blk = key of this block
-        const bool ok = kb * 32 + blk < a.Nk;   // keys past the end: P2 = dS = 0
+        const bool ok = kb * 32 + blk < a.Nk;   // keys past the end: P2 = dS = 0 (wave-uniform)
+        if (ok) {
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {   // dp[u] becomes dS1 in place
-          p[u][r] = ok ? ex2(__builtin_fmaf(p[u][r], kLog2e, -lse2[r])) : 0.f;
-          dp[u][r] = p[u][r] * (dp[u][r] - dl[r]);
+          for (int r = 0; r < NR; ++r) {   // dp[u] becomes dS1 in place
+            p[u][r] = ex2(p[u][r] - lse2[r]);
+            dp[u][r] = p[u][r] * (dp[u][r] - dl[r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < NR; ++r) p[u][r] = dp[u][r] = 0.f;
         }
         if constexpr (!KST) {
 #pragma unroll
