@@ -454,11 +454,11 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
 
 // bf16 with the head mixes on the MFMA (th2.h).  H <= 8: one wave per head (NWMAX 8).  9..16 heads:
 // two heads per wave (eight waves of <= 256 registers; sixteen waves of 128 spilled heavily).
-template <int DP, int NWMAX, bool ROT, int HPW> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
+template <int DP, int NWMAX, bool ROT, int HPW, bool LEAN = false> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32, nw = (a.H + HPW - 1) / HPW;
   const size_t lds = th2_lds_bytes<DP, NWMAX * HPW <= 8>(a.H);
-  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW>, lds)) return rc;
-  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
+  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>, lds)) return rc;
+  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   return check_launch("th2_fwd");
 }
 
@@ -477,9 +477,11 @@ template <int DP, int NWMAX, bool ROT, int HPW> int th2_bwd_run(hipStream_t st, 
   return check_launch("th_reduce");
 }
 
+// <= 8 heads: the forward at <= 128 VGPRs, two workgroups per CU (CaiT-S24 207 -> 184 us,
+// profiles/r05v_th_lean_ab.txt)
 template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
-  if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true, 1>(st, a) : th2_fwd_run<DP, 8, true, 2>(st, a);
-  return a.H <= 8 ? th2_fwd_run<DP, 8, false, 1>(st, a) : th2_fwd_run<DP, 8, false, 2>(st, a);
+  if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true, 1, true>(st, a) : th2_fwd_run<DP, 8, true, 2>(st, a);
+  return a.H <= 8 ? th2_fwd_run<DP, 8, false, 1, true>(st, a) : th2_fwd_run<DP, 8, false, 2>(st, a);
 }
 template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
   if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true, 1>(st, a) : th2_bwd_run<DP, 8, true, 2>(st, a);

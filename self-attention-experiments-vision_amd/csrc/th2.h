@@ -226,8 +226,10 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
 // the score tile's MFMA results before the mixes can start, so nothing overlapped.)
 // HPW heads per wave (1, or 2 for 9..16 heads: eight waves of up to 256 registers instead of
 // sixteen of 128, which spilled); wave w owns heads w + NW e, e < HPW, NW = ceil(H / HPW) waves.
-template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
-__global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
+// LEAN: <= 128 VGPRs (four waves per SIMD: two workgroups per CU at <= 8 heads) -- no K prefetch,
+// mix groups of two
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1, bool LEAN = false>
+__global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
   constexpr int NS = DP / 16, NT = DP / 32;
   constexpr bool KST = NWMAX * HPW <= 8;     // H <= 8: stacked mixes, heads in registers 0..3
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   // would otherwise sit in front of every tile's first MFMA)
   // one head per wave: the next key tile's K fragments are in flight while this one computes; two
   // heads: the registers hold the second head's Q instead and each head's K loads directly
-  constexpr bool PF = HPW == 1;
+  constexpr bool PF = HPW == 1 && !LEAN;
   bf16x8 kn[NS];
   auto load_k = [&](int e, int kt) {
 #pragma unroll
@@ -311,13 +313,14 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       if (hv[e]) th2_put(XS, hd[e], s, a.scale, lane);
     }
   };
-  auto stats = [&](int kt) {   // this wave's blocks of tile kt, groups of four: one max update each
+  auto stats = [&](int kt) {   // this wave's blocks of tile kt, groups of SG: one max update each
+    constexpr int SG = LEAN ? 2 : 4;
     const char* xs = XS;
-    for (int b0 = w; b0 < 32; b0 += 4 * NW) {
-      f32x16 c[4];
-      bool ok[4];
+    for (int b0 = w; b0 < 32; b0 += SG * NW) {
+      f32x16 c[SG];
+      bool ok[SG];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {   // independent chains: issued together, blocks past the end clamped
+      for (int u = 0; u < SG; ++u) {   // independent chains: issued together, blocks past the end clamped
         const int blk = b0 + u * NW;
         ok[u] = blk < 32 && kt * 32 + blk < a.Nk;
         c[u] = th2_mix_img<KST>(xs, blk & 31, m1, lane);
@@ -327,12 +330,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
       for (int r = 0; r < NR; ++r) {
         float mx = -kInf;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < SG; ++u)
           if (ok[u]) mx = fmaxf(mx, c[u][r]);
         const float mn = fmaxf(m[r], mx);
         float sum = l[r] * ex2(m[r] - mn);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < SG; ++u)
           if (ok[u]) sum += ex2(c[u][r] - mn);
         l[r] = sum;
         m[r] = mn;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_fwd_kernel(ThArgs a) {
   auto probs = [&](int kt) {   // this wave's blocks of tile kt: P2 = T2^T P into XP
     const char* xs = XS;
     char* xp = XP;
-    constexpr int G = KST ? 4 : 2;   // blocks per group: independent chains issued together
+    constexpr int G = KST && !LEAN ? 4 : 2;   // blocks per group: independent chains issued together
     const bool whole = kt * 32 + 32 <= a.Nk;   // every key of the tile exists (wave-uniform)
     for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 c[G];
