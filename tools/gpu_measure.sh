@@ -15,7 +15,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -k 10 300 python3 tools/attn_bench.py --iters 20 > gpurun_out/${tag}_attn_bench.txt 2>&1
 timeout -k 10 300 python3 tools/attn_bench.py --shapes bot14,bot7 --rel --iters 20 >> gpurun_out/${tag}_attn_bench.txt 2>&1
 timeout -k 10 300 python3 tools/attn_bench.py --shapes cait_s24,cait_m24 --th --iters 20 >> gpurun_out/${tag}_attn_bench.txt 2>&1
-tools/pmc.sh gpurun_out/${tag}_pmc_train python3 bench.py --profile --eager --steps 3 --warmup 2
 tools/pmc.sh gpurun_out/${tag}_pmc_b384 python3 tools/attn_bench.py --shapes vitb384 --iters 3
 tools/pmc.sh gpurun_out/${tag}_pmc_th python3 tools/attn_bench.py --shapes cait_s24 --th --iters 3
+tools/pmc.sh gpurun_out/${tag}_pmc_th_m24 python3 tools/attn_bench.py --shapes cait_m24 --th --iters 3
+tools/pmc.sh gpurun_out/${tag}_pmc_deit python3 tools/attn_bench.py --shapes deit_s --iters 3
 echo ALL_DONE
