@@ -689,9 +689,11 @@ static bool g8x_route(int M, int N, int K, int epilogue) {
 // Round 4 (224-row tiles, g8_pick_bm): also the DeiT-S / CaiT wide K = 384 outputs -- QKV forward
 // 593 -> 647 TF/s, FF Dense_0 + GELU 546 -> 563, Dense_1 input gradient with GELU' 497 -> 509
 // (profiles/r04k_g8probe.txt, v53 vs rel)
-static bool g8_route(int M, int N, int K, int epilogue) {
+// Round 5: with the saved-gelu' multiply epilogue (SAE_EPI_MUL_AUX, `gp`) the GELU' epilogue no
+// longer bounds the deeper ViT-B input gradient either, so gemm8 takes it at every K.
+static bool g8_route(int M, int N, int K, int epilogue, bool gp = false) {
   if (N % 192 || K % 64 || K < 384 || M < 4096) return false;
-  return epilogue != SAE_EPI_DGELU || K == 384;
+  return epilogue != SAE_EPI_DGELU || K == 384 || (gp && !dev_knob("SAE_G8_NO_MUL"));
 }
 
 extern "C" {
@@ -1300,9 +1302,10 @@ int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, 
 int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
   if (M < 1 || N < 1 || K < 1 || K % 8 || N % 8 || epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_MUL_AUX)
     return SAE_NT_ROUTE_NONE;
-  if (epilogue >= SAE_EPI_GELU_GRAD) epilogue -= 2;   // the gelu' forms run on the GELU / GELU' kernels
+  const bool gp = epilogue >= SAE_EPI_GELU_GRAD;
+  if (gp) epilogue -= 2;   // the gelu' forms run on the GELU / GELU' kernels
   if (g8x_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8X;
-  if (g8_route(M, N, K, epilogue)) return SAE_NT_ROUTE_GEMM8;
+  if (g8_route(M, N, K, epilogue, gp)) return SAE_NT_ROUTE_GEMM8;
   return K % kNtK ? SAE_NT_ROUTE_TILE128_KTAIL : SAE_NT_ROUTE_TILE128;
 }
 
@@ -1353,7 +1356,7 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
     if (rc) return rc;
     return check_launch("gemm8x_nt");
   }
-  if (g8_route(M, N, K, epilogue)
+  if (g8_route(M, N, K, epilogue, gp)
 #ifdef SAE_DEV_KNOBS
       && !dev_knob("SAE_NT_NO_G8")
 #endif
