@@ -1617,8 +1617,11 @@ int sae_weight_cast_multi(void* stream, int32_t n, const sae_weight_cast_item* i
 }
 
 // ------------------------------------------------------------ residual add + LayerNorm
-static int ln_fwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 2048)); }
-static int ln_bwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 1024)); }
+// rows per wave: with the rows software-pipelined (ln.h) fewer, longer-lived waves win -- 2048 / 1024
+// -> 1024 / 512 workgroups: DeiT-S step 8.220 -> 8.174 ms same box (profiles/r05ac_ln_grid_ab.txt;
+// before the pipelining, 512 backward workgroups were slower: too few rows in flight)
+static int ln_fwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 1024)); }
+static int ln_bwd_blocks(int M) { return std::max(1, std::min((M + 3) / 4, 512)); }
 
 static int ln_check(int32_t M, int32_t C) {
   if (M < 1 || C < 4) return fail(SAE_EINVAL, "layernorm: M (%d) and C (%d) must be >= 1 / >= 4", M, C);
@@ -1674,7 +1677,11 @@ static int ln_fwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
   a.rsc = rsc;
   a.rpb = rpb > 0 ? rpb : 1;
   const int nv = (C / 4 + 63) / 64;
-  const dim3 g(ln_fwd_blocks(M)), b(256);
+  int lnb = ln_fwd_blocks(M);
+#ifdef SAE_DEV_KNOBS
+  if (int v = dev_knob("SAE_LN_FWD_BLOCKS")) lnb = std::max(1, std::min((M + 3) / 4, v));
+#endif
+  const dim3 g(lnb), b(256);
   hipStream_t st = (hipStream_t)stream;
   switch (nv) {
     case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, g, b, 0, st, a); break;
@@ -1931,6 +1938,9 @@ static int ln_bwd_impl(void* stream, int32_t M, int32_t C, const float* x, const
   a.M = M;
   a.C = C;
   a.nblk = ln_bwd_blocks(M);
+#ifdef SAE_DEV_KNOBS
+  if (int v = dev_knob("SAE_LN_BWD_BLOCKS")) a.nblk = std::max(1, std::min(a.nblk, v));   // (workspace: <= default)
+#endif
   a.delta = reinterpret_cast<const __bf16*>(delta);
   a.lsc = lsc;
   a.rsc = rsc;
