@@ -105,10 +105,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
       nd[k] = (hasd && c < C4) ? *reinterpret_cast<const bf16x4*>(a.delta + ro + 4 * c) : bf16x4{};
     }
   };
-  if (wave < a.M) load(wave);
+  float nsf = 1.f;
+  if (wave < a.M) {
+    load(wave);
+    if (a.rsc) nsf = a.rsc[wave / a.rpb];
+  }
   for (int row = wave; row < a.M; row += nw) {
     const size_t ro = (size_t)row * a.C;
-    const float rsf = a.rsc ? a.rsc[row / a.rpb] : 1.f;
+    const float rsf = nsf;
     f32x4 v[NV];
     bf16x4 dv[NV];
 #pragma unroll
@@ -116,7 +120,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
       v[k] = nx[k];
       dv[k] = nd[k];
     }
-    if (row + nw < a.M) load(row + nw);
+    if (row + nw < a.M) {
+      load(row + nw);
+      if (a.rsc) nsf = a.rsc[(row + nw) / a.rpb];
+    }
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -169,34 +176,37 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
   }
   const float invC = 1.f / (float)a.C;
   const bool hasin = a.dxin != nullptr;
-  // the next row's dy / x / dx_in (and mean / rstd), in flight during this row (as ln_fwd_kernel)
-  bf16x4 ndy[NV];
+  // the next row's dy / x / dx_in (and mean / rstd; NP = 3: delta and the row scale), in flight
+  // during this row (as ln_fwd_kernel)
+  bf16x4 ndy[NV], nde[NP == 3 ? NV : 1];
   f32x4 nx[NV], ni[NV];
-  float nmu = 0.f, nrs = 0.f;
+  float nmu = 0.f, nrs = 0.f, nsf = 1.f;
   auto load = [&](int row) {
     const size_t ro = (size_t)row * a.C;
     nmu = a.mean[row];
     nrs = a.rstd[row];
+    if constexpr (NP == 3) nsf = a.rsc ? a.rsc[row / a.rpb] : 1.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = lane + 64 * k;
       ndy[k] = c < C4 ? *reinterpret_cast<const bf16x4*>(a.dy + ro + 4 * c) : bf16x4{};
       nx[k] = c < C4 ? reinterpret_cast<const f32x4*>(a.x + ro)[c] : f32x4{};
       ni[k] = (hasin && c < C4) ? reinterpret_cast<const f32x4*>(a.dxin + ro)[c] : f32x4{};
+      if constexpr (NP == 3) nde[k] = c < C4 ? *reinterpret_cast<const bf16x4*>(a.delta + ro + 4 * c) : bf16x4{};
     }
   };
   if (wave < a.M) load(wave);
   for (int row = wave; row < a.M; row += nw) {
     const size_t ro = (size_t)row * a.C;
-    const float mu = nmu, rs = nrs;
-    const float rsf = (NP == 3 && a.rsc) ? a.rsc[row / a.rpb] : 1.f;
+    const float mu = nmu, rs = nrs, rsf = nsf;
     f32x4 xh[NV], gy[NV], din[NV];
-    bf16x4 dyr[NV];
+    bf16x4 dyr[NV], der[NP == 3 ? NV : 1];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       dyr[k] = ndy[k];
       xh[k] = nx[k];
       din[k] = ni[k];
+      if constexpr (NP == 3) der[k] = nde[k];
     }
     if (row + nw < a.M) load(row + nw);
     float s1 = 0.f, s2 = 0.f;
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
         if (hasin) d += din[k];
         reinterpret_cast<f32x4*>(a.dx + ro)[c] = d;
         if constexpr (NP == 3) {   // x_out = x + delta * ls * rsf
-          pl[k] += d * ld_bf16x4(a.delta + ro + 4 * c) * rsf;
+          pl[k] += d * f32x4{(float)der[k][0], (float)der[k][1], (float)der[k][2], (float)der[k][3]} * rsf;
           if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d * ls[k] * rsf);
         } else {
           if (a.ddelta) st_bf16x4(a.ddelta + ro + 4 * c, d);
