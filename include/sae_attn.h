@@ -277,6 +277,13 @@ int sae_patch_embed_fwd(void* stream, const sae_patch_desc* desc, const void* im
 size_t sae_patch_embed_bwd_workspace_bytes(const sae_patch_desc* desc);
 int sae_patch_embed_bwd(void* stream, const sae_patch_desc* desc, const void* images,
                         const void* dout, float* dw, float* db, int32_t accumulate, void* workspace);
+/* The patch matrix of HWCN images as bf16 rows: patches[n * L + p][k], k = (ky * Pw + kx) * C + c
+   (the einops order of patch_embed.py:21), L = (H / Ph) * (W / Pw), K = Ph * Pw * C; fp32 images
+   are rounded to bf16 (the same operand bits as sae_patch_embed_fwd's loaders).  The train step
+   writes it once and runs the embedding as sae_gemm_nt(patches, W^T) and its weight gradient as
+   sae_gemm_dw(patches, dY): the LDS-DMA GEMM kernels instead of the per-chunk eight-image scatter of
+   the fused HWCN loaders.  desc as sae_patch_embed_fwd, layout SAE_LAYOUT_HWCN. */
+int sae_patch_gather(void* stream, const sae_patch_desc* desc, const void* images, void* patches);
 
 /* Residual add + LayerNorm of the encoder blocks around the path (models/vit.py:19-31,57;
    Flax nn.LayerNorm: fp32 statistics, eps, output in the compute dtype):

@@ -76,6 +76,7 @@ _PROTOS = [
     ("sae_patch_embed_fwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp]),
     ("sae_patch_embed_bwd_workspace_bytes", _sz, [ctypes.POINTER(SaePatchDesc)]),
     ("sae_patch_embed_bwd", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp, _vp, _vp, _i32, _vp]),
+    ("sae_patch_gather", _i32, [_vp, ctypes.POINTER(SaePatchDesc), _vp, _vp]),
     ("sae_weight_cast", _i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
     ("sae_weight_cast_multi", _i32, [_vp, _i32, _vp]),
     ("sae_layernorm_fwd", _i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32]),

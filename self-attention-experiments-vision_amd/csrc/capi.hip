@@ -1509,6 +1509,25 @@ int sae_patch_embed_fwd(void* stream, const sae_patch_desc* d, const void* image
   return rc ? rc : ok();
 }
 
+int sae_patch_gather(void* stream, const sae_patch_desc* d, const void* images, void* patches) {
+  PatchGeom g;
+  int M, K;
+  if (int rc = patch_geom(d, &g, &M, &K)) return rc;
+  if (d->layout != SAE_LAYOUT_HWCN) return fail(SAE_EUNSUPPORTED, "patch_gather: HWCN images only");
+  if (!images || !patches) return fail(SAE_EINVAL, "patch_gather: images / patches must be non-NULL");
+  if (!aligned16(images) || !aligned16(patches))
+    return fail(SAE_EINVAL, "patch_gather: images and patches must be 16-byte aligned");
+  g.x = images;
+  const dim3 grid((unsigned)g.L, (unsigned)((g.Nb + 63) / 64), (unsigned)((K / 8 + 3) / 4));
+  if (d->dtype == SAE_DTYPE_F32)
+    hipLaunchKernelGGL(patch_gather_hwcn_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, g,
+                       reinterpret_cast<__bf16*>(patches), K);
+  else
+    hipLaunchKernelGGL(patch_gather_hwcn_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, g,
+                       reinterpret_cast<__bf16*>(patches), K);
+  return check_launch("patch_gather");
+}
+
 size_t sae_patch_embed_bwd_workspace_bytes(const sae_patch_desc* d) {
   PatchGeom g;
   int M, K;

@@ -222,4 +222,29 @@ struct DwPermY {
   }
 };
 
+
+// The patch matrix itself (round 5, HWCN train-step feed): A[n L + p][k] bf16 written once, so the
+// embedding GEMM and its weight gradient run on the LDS-DMA kernels (gemm8 / gemm_dw8) instead of
+// gathering eight images per 16-byte chunk into eight operand rows (the fused HWCN loaders ran the
+// 25,088 x 768 x 384 product at 1.3 TB/s of image reads, 59 + 56 us at DeiT-S).  Thread (n, kg)
+// reads image elements k = 8 kg .. 8 kg + 7 of token row (n, p) -- for one k, consecutive n are
+// consecutive addresses, so a wave's loads are whole 256-byte runs -- rounds them to bf16 (as the
+// fused loaders do: the same operand bits) and stores one 16-byte chunk of the row.
+template <bool F32>
+__global__ __launch_bounds__(256) void patch_gather_hwcn_kernel(PatchGeom g, __bf16* out, int K) {
+  const int kgs = K / 8;
+  const int n = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int kg = blockIdx.z * 4 + (threadIdx.x >> 6);
+  const int p = blockIdx.x;
+  if (n >= g.Nb || kg >= kgs) return;
+  const unsigned base = patch_rowbase<true>(g, p * g.Nb + n);
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned e = base + patch_kofs<true>(g, 8 * kg + j);
+    v[j] = F32 ? (__bf16)reinterpret_cast<const float*>(g.x)[e] : reinterpret_cast<const __bf16*>(g.x)[e];
+  }
+  *reinterpret_cast<bf16x8*>(out + ((long long)n * g.L + p) * K + 8 * kg) = v;
+}
+
 }  // namespace sae

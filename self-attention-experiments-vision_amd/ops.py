@@ -970,10 +970,19 @@ def _patch_desc(images: torch.Tensor, patch: Tuple[int, int], embed: int, layout
     return L.SaePatchDesc(B, H, W, C, int(patch[0]), int(patch[1]), int(embed), code, dtype_code(images.dtype))
 
 
+# HWCN images (the train-step feed): write the patch matrix once (sae_patch_gather) and run the
+# embedding and its weight gradient on the LDS-DMA GEMMs -- DeiT-S 59 + 56 us of fused HWCN
+# gathers against the gather + gemm8 + gemm_dw8 (profiles/r05af_patch_gather_ab.txt).  False: the
+# fused loaders (no patch copy; A/B runs).
+PATCH_GATHER = os.environ.get("SAE_PATCH_GATHER", "1") != "0"
+
+
 class _PatchEmbed(torch.autograd.Function):
     """patch_embed.py:15-26 in bf16: the patch gather fused into the GEMM's operand staging
-    (``sae_patch_embed_fwd``), weight / bias gradients by the same gather (``sae_patch_embed_bwd``).
-    The images take no gradient (they are the batch, train.py:80-82)."""
+    (``sae_patch_embed_fwd``), weight / bias gradients by the same gather (``sae_patch_embed_bwd``);
+    for HWCN images the patch matrix is written once (``sae_patch_gather``) and both products run on
+    ``sae_gemm_nt`` / ``sae_gemm_dw``.  The images take no gradient (they are the batch,
+    train.py:80-82)."""
 
     @staticmethod
     def forward(ctx, images, w, b, patch, layout):
@@ -982,15 +991,24 @@ class _PatchEmbed(torch.autograd.Function):
         desc = _patch_desc(images, patch, E, layout)
         _, wt = _cast([w], torch.bfloat16)
         Lp = (desc.height // desc.patch_h) * (desc.width // desc.patch_w)
-        out = torch.empty((desc.batch, Lp, E), dtype=torch.bfloat16, device=images.device)
+        K = desc.patch_h * desc.patch_w * desc.channels
         bias = b.float().contiguous() if b is not None else None
         tok = _TIMER.begin("patch_embed") if _TIMER is not None else None
-        L.check(lib.sae_patch_embed_fwd(_stream(images), ctypes.byref(desc), _ptr(images), _ptr(wt), _ptr(bias),
-                                        _ptr(out)))
+        gathered = layout == "HWCN" and PATCH_GATHER and E % 8 == 0
+        if gathered:
+            pm = torch.empty((desc.batch * Lp, K), dtype=torch.bfloat16, device=images.device)
+            L.check(lib.sae_patch_gather(_stream(images), ctypes.byref(desc), _ptr(images), _ptr(pm)))
+            out = gemm_nt(pm, wt, bias).view(desc.batch, Lp, E)
+            ctx.save_for_backward(pm)
+        else:
+            out = torch.empty((desc.batch, Lp, E), dtype=torch.bfloat16, device=images.device)
+            L.check(lib.sae_patch_embed_fwd(_stream(images), ctypes.byref(desc), _ptr(images), _ptr(wt),
+                                            _ptr(bias), _ptr(out)))
+            ctx.save_for_backward(images)
         if tok is not None:
             _TIMER.end(tok, (desc.batch * Lp, w.shape[0], E))
-        ctx.save_for_backward(images)
         ctx.desc, ctx.wshape, ctx.wdtype, ctx.has_b = desc, tuple(w.shape), w.dtype, b is not None
+        ctx.gathered = gathered
         ctx.sinks = (_sink(w), _sink(b))
         return out
 
@@ -998,17 +1016,20 @@ class _PatchEmbed(torch.autograd.Function):
     @_sinking
     def backward(ctx, dout):
         lib = L.load()
-        (images,) = ctx.saved_tensors
+        (saved,) = ctx.saved_tensors
         desc = ctx.desc
         dout = dout.to(torch.bfloat16).contiguous()
         sw, sb = ctx.sinks   # flat-buffer sinks (multi-rank step): written in place
         dw = _claim(sw) if sw is not None else torch.empty(ctx.wshape, dtype=torch.float32, device=dout.device)
         db = _claim(sb) if sb is not None else (
             torch.empty((ctx.wshape[1],), dtype=torch.float32, device=dout.device) if ctx.has_b else None)
-        ws = torch.empty(lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8,
-                         device=dout.device)
-        L.check(lib.sae_patch_embed_bwd(_stream(dout), ctypes.byref(desc), _ptr(images), _ptr(dout), _ptr(dw),
-                                        _ptr(db), 0, _ptr(ws)))
+        if ctx.gathered:   # dW = P^T dY, db = colsum(dY) on the weight-gradient kernel
+            gemm_dw(saved, dout.view(-1, ctx.wshape[1]), dw, db)
+        else:
+            ws = torch.empty(lib.sae_patch_embed_bwd_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8,
+                             device=dout.device)
+            L.check(lib.sae_patch_embed_bwd(_stream(dout), ctypes.byref(desc), _ptr(saved), _ptr(dout), _ptr(dw),
+                                            _ptr(db), 0, _ptr(ws)))
         return None, None if sw is not None else dw.to(ctx.wdtype), _unsunk(db, sb), None, None
 
 

@@ -111,3 +111,45 @@ def test_vit_forward_layouts(dev, layout):
         y = m(feed, is_training=False, layout=layout)
         y_nhwc = m(img, is_training=False)
     assert torch.equal(y, y_nhwc)
+
+
+@pytest.mark.parametrize("idt", [torch.bfloat16, torch.float32])
+def test_patch_gather_hwcn_exact(dev, idt):
+    """sae_patch_gather writes the patch matrix of an HWCN feed bit for bit: rows n L + p, columns
+    (ky Pw + kx) C + c, each image value rounded to bf16 (oracle: vit_ref.patchify of the NHWC view)."""
+    import ctypes
+    import sae_vision_amd.ops as ops
+    from sae_vision_amd import _lib as L
+    B, H, W, C, ph, pw, E = 16, 64, 48, 3, 16, 16, 384
+    g = torch.Generator(device=dev).manual_seed(11)
+    img = torch.randn(B, H, W, C, device=dev, generator=g).to(idt)
+    feed = img.permute(1, 2, 3, 0).contiguous()
+    desc = ops._patch_desc(feed, (ph, pw), E, "HWCN")
+    Lp, K = (H // ph) * (W // pw), ph * pw * C
+    pm = torch.empty((B * Lp, K), dtype=torch.bfloat16, device=dev)
+    L.check(L.load().sae_patch_gather(ops._stream(feed), ctypes.byref(desc), ops._ptr(feed), ops._ptr(pm)))
+    ref = vit_ref.patchify(img.to(torch.bfloat16).float().cpu().numpy(), (ph, pw)).reshape(B * Lp, K)
+    assert np.array_equal(pm.float().cpu().numpy(), ref)
+
+
+def test_patch_embed_gathered_vs_fused(dev, monkeypatch):
+    """The DeiT-S stem (M = 25,088 token rows: gemm8 / gemm_dw8 on the gathered patch matrix) against
+    the fused HWCN loaders: the same bf16 operands, so outputs agree to bf16 rounding and dW to
+    fp32 summation order."""
+    import sae_vision_amd.ops as ops
+    g = torch.Generator(device=dev).manual_seed(12)
+    B, H, W, C, E = 128, 224, 224, 3, 384
+    feed = torch.randn(H, W, C, B, device=dev, generator=g)
+    w = (torch.randn(768, E, device=dev, generator=g) / 768 ** 0.5).requires_grad_(True)
+    b = (torch.randn(E, device=dev, generator=g) * 0.1).requires_grad_(True)
+    dy = torch.randn(B, 196, E, device=dev, generator=g).to(torch.bfloat16)
+    outs = {}
+    for gathered in (True, False):
+        monkeypatch.setattr(ops, "PATCH_GATHER", gathered)
+        w.grad = b.grad = None
+        y = ops.patch_embed(feed, w, b, (16, 16), "HWCN")
+        y.backward(dy)
+        outs[gathered] = (y.detach().float(), w.grad.clone(), b.grad.clone())
+    (y1, dw1, db1), (y0, dw0, db0) = outs[True], outs[False]
+    assert _rel(y1, y0) < 1e-2
+    assert _rel(dw1, dw0) < 1e-4 and _rel(db1, db0) < 1e-4
