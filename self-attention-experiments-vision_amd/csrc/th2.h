@@ -42,8 +42,13 @@ constexpr int kTh2Row = 32 * kTh2Blk + 64;       // bytes per head row (2624 = 1
 // KST ("K-stacked", H <= 8): a mix is ONE MFMA whose K = 16 holds the 8 heads twice, the high
 // bf16 part of T against the first copy and the low part against the second, and the images
 // need only 8 rows; otherwise (H <= 16) two MFMAs (high, low) over 16 image rows.
+// Row r starts at th2_ro(r): rows 4-7 and 12-15 sit 32 bytes (8 banks) further, so that the dT
+// reads (ds_read_b128, one 16-byte piece of each of 8 / 16 rows in a 16-lane group) find rows r
+// and r + 4 on different banks (2-way conflicts with a uniform stride); the mixes' transposed
+// reads take rows 0-3 and 4-7 in separate instructions, so the shift costs them nothing.
 template <bool KST> constexpr int th2_rows() { return KST ? 8 : kTh2MaxH; }
-template <bool KST> constexpr int th2_img() { return th2_rows<KST>() * kTh2Row; }   // one exchange image
+__host__ __device__ constexpr int th2_ro(int r) { return r * kTh2Row + 32 * ((r >> 2) & 1); }
+template <bool KST> constexpr int th2_img() { return th2_rows<KST>() * kTh2Row + 32; }   // one exchange image
 constexpr int kTh2MixTbl = 4 * 64 * 32;          // th2_bwd_kv: four mix operands (hi, lo) per lane
 
 typedef __attribute__((ext_vector_type(8))) short th_s16x8;
@@ -63,6 +68,15 @@ __device__ __forceinline__ bf16x8 th2_tr2(const char* p1, const char* p2) {
 struct Th2Mix {
   bf16x8 hi, lo;
 };
+// n mix operands per lane in LDS: the high parts of all n, then the low parts -- a 16-byte lane
+// stride (conflict-free ds_read_b128; {hi, lo} pairs at a 32-byte stride conflicted 2-way)
+__device__ __forceinline__ void th2_mx_put(char* t, int n, int k, int lane, const Th2Mix& m) {
+  reinterpret_cast<bf16x8*>(t)[k * 64 + lane] = m.hi;
+  reinterpret_cast<bf16x8*>(t)[(n + k) * 64 + lane] = m.lo;
+}
+__device__ __forceinline__ Th2Mix th2_mx_get(const char* t, int n, int k, int lane) {
+  return Th2Mix{reinterpret_cast<const bf16x8*>(t)[k * 64 + lane], reinterpret_cast<const bf16x8*>(t)[(n + k) * 64 + lane]};
+}
 // `mul` scales T before the split (th2_fwd: log2 e, so the mixed logits come out in the log2 domain)
 template <bool TR, bool PERM, bool KST>
 __device__ __forceinline__ Th2Mix th2_mix(const float* T, int H, int lane, float mul = 1.f) {
@@ -92,7 +106,7 @@ __device__ __forceinline__ f32x16 th2_mix_img(const char* img, int blk, const Th
   const int li = lane & 15;
   const int r1 = (KST ? 0 : 8 * (lane >> 5)) + (li >> 2);   // KST: both lane halves read rows 0..7
   const int col = blk * kTh2Blk + (16 * ((lane >> 4) & 1) + 4 * (li & 3)) * 2;
-  const bf16x8 b = th2_tr2(img + r1 * kTh2Row + col, img + (r1 + 4) * kTh2Row + col);
+  const bf16x8 b = th2_tr2(img + th2_ro(r1) + col, img + th2_ro(r1 + 4) + col);
   const f32x16 c = MF<__bf16>::mma(m.hi, b, zero16());
   if constexpr (KST) return c;
   return MF<__bf16>::mma(m.lo, b, c);
@@ -126,7 +140,7 @@ __device__ __forceinline__ f32x16 th2_mix_acc(const f32x16& x, const Th2Mix& m) 
 // the lane) into image row `head` at position key * 32 + query: registers 4g .. 4g + 3 are four
 // consecutive positions, one 8-byte write
 __device__ __forceinline__ void th2_put(char* img, int head, const f32x16& v, float sc, int lane) {
-  char* p = img + head * kTh2Row + (lane & 31) * kTh2Blk + 8 * (lane >> 5);
+  char* p = img + th2_ro(head) + (lane & 31) * kTh2Blk + 8 * (lane >> 5);
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 #pragma unroll
   for (int g = 0; g < 4; ++g)
@@ -142,21 +156,21 @@ __device__ __forceinline__ void th2_put_block(char* img, int blk, const f32x16& 
   const int h = lane >> 5;
   if (H >= 2 * NR) {   // every row of the registers is a head (wave-uniform): no per-lane branches
 #pragma unroll
-    for (int r = 0; r < NR; ++r) *reinterpret_cast<__bf16*>(p + row_of(r, h) * kTh2Row) = (__bf16)v[r];
+    for (int r = 0; r < NR; ++r) *reinterpret_cast<__bf16*>(p + th2_ro(row_of(r, h))) = (__bf16)v[r];
     return;
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int i = row_of(r, h);
-    if (i < H) *reinterpret_cast<__bf16*>(p + i * kTh2Row) = (__bf16)v[r];
+    if (i < H) *reinterpret_cast<__bf16*>(p + th2_ro(i)) = (__bf16)v[r];
   }
 }
 
 // zero image rows [H, rows) once (read as the padded k of the mixes; must be finite)
 template <bool KST>
 __device__ __forceinline__ void th2_zero_pad(char* img, int H, int tid, int nthreads) {
-  uint4* p = reinterpret_cast<uint4*>(img + H * kTh2Row);
-  const int n = (th2_rows<KST>() - H) * kTh2Row / 16;
+  uint4* p = reinterpret_cast<uint4*>(img + th2_ro(H));
+  const int n = (th2_img<KST>() - th2_ro(H)) / 16;
   for (int i = tid; i < n; i += nthreads) p[i] = uint4{0, 0, 0, 0};
 }
 
@@ -166,8 +180,8 @@ template <bool KST>
 __device__ __forceinline__ f32x4 th2_dt(const char* ia, const char* ib, int blk, f32x4 acc, int lane) {
   // KST: 8-row images; lanes 8..15 re-read rows 0..7 (their dT rows / columns are discarded)
   const int row = lane & (KST ? 7 : 15), o = blk * kTh2Blk + 16 * (lane >> 4);
-  const bf16x8 a = *reinterpret_cast<const bf16x8*>(ia + row * kTh2Row + o);
-  const bf16x8 b = *reinterpret_cast<const bf16x8*>(ib + row * kTh2Row + o);
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(ia + th2_ro(row) + o);
+  const bf16x8 b = *reinterpret_cast<const bf16x8*>(ib + th2_ro(row) + o);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
@@ -179,7 +193,7 @@ __device__ __forceinline__ bf16x8 th2_colB(const char* img, int head, int s, int
   const int li = lane & 15;
   const int r1 = 16 * s + 4 * (lane >> 5) + (li >> 2);
   const int col = (16 * ((lane >> 4) & 1) + 4 * (li & 3)) * 2;
-  const char* base = img + head * kTh2Row + col;
+  const char* base = img + th2_ro(head) + col;
   return th2_tr2(base + r1 * kTh2Blk, base + (r1 + 8) * kTh2Blk);
 }
 
@@ -195,7 +209,7 @@ __device__ __forceinline__ bf16x8 th2_frag(__amdgpu_buffer_rsrc_t rsrc, int row,
 // th2_rowB: image row `head` read as a [column = lane][row] matrix (position = column * 32 + row:
 // the key-block kernel, B[k = query][column = key]): two 8-byte reads of query runs
 __device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int lane) {
-  const char* base = img + head * kTh2Row + (lane & 31) * kTh2Blk + (16 * s + 4 * (lane >> 5)) * 2;
+  const char* base = img + th2_ro(head) + (lane & 31) * kTh2Blk + (16 * s + 4 * (lane >> 5)) * 2;
   const s16x4 x1 = *reinterpret_cast<const s16x4*>(base);
   const s16x4 x2 = *reinterpret_cast<const s16x4*>(base + 16);
   const th_s16x8 v = {x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
@@ -509,19 +523,19 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   // the mix operands: registers (one head per wave) or, with two heads per wave, an LDS table that
   // wave 0 writes before the first barrier (the registers go to the second head's operands)
   Th2Mix m1r, m2tr, m1tr;
-  Th2Mix* const mxt = reinterpret_cast<Th2Mix*>(smem + 2 * IMG + H * I::bytes(32));
+  char* const mxt = smem + 2 * IMG + H * I::bytes(32);
   if constexpr (HPW == 1) {
     m1r = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);   // S1 = T1^T S, log2 domain (image)
     m2tr = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
     m1tr = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
   } else if (w == 0) {
-    mxt[lane] = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);
-    mxt[64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);
-    mxt[128 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);
+    th2_mx_put(mxt, 3, 0, lane, th2_mix<false, false, KST>(a.th1, H, lane, kLog2e));
+    th2_mx_put(mxt, 3, 1, lane, th2_mix<true, false, KST>(a.th2, H, lane));
+    th2_mx_put(mxt, 3, 2, lane, th2_mix<true, true, KST>(a.th1, H, lane));
   }
-  auto m1 = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1r; else return mxt[lane]; };
-  auto m2t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m2tr; else return mxt[64 + lane]; };
-  auto m1t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1tr; else return mxt[128 + lane]; };
+  auto m1 = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1r; else return th2_mx_get(mxt, 3, 0, lane); };
+  auto m2t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m2tr; else return th2_mx_get(mxt, 3, 1, lane); };
+  auto m1t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1tr; else return th2_mx_get(mxt, 3, 2, lane); };
   // lse (log2 domain) of the mixed rows of this lane's query, register r <-> head row_of(r, h)
   float lse2[NR];
 #pragma unroll
@@ -767,13 +781,12 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   };
   if constexpr (KVR) load_kv(0);
   if (w == 0) {
-    Th2Mix* mx = reinterpret_cast<Th2Mix*>(MX);
-    mx[0 * 64 + lane] = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);   // log2 e T1^T, image operand
-    mx[1 * 64 + lane] = th2_mix<false, true, KST>(a.th2, H, lane);    // T2^T, accumulator operand
-    mx[2 * 64 + lane] = th2_mix<true, false, KST>(a.th2, H, lane);    // T2, image operand
-    mx[3 * 64 + lane] = th2_mix<true, true, KST>(a.th1, H, lane);     // T1, accumulator operand
+    th2_mx_put(MX, 4, 0, lane, th2_mix<false, false, KST>(a.th1, H, lane, kLog2e));   // log2 e T1^T, image operand
+    th2_mx_put(MX, 4, 1, lane, th2_mix<false, true, KST>(a.th2, H, lane));    // T2^T, accumulator operand
+    th2_mx_put(MX, 4, 2, lane, th2_mix<true, false, KST>(a.th2, H, lane));    // T2, image operand
+    th2_mx_put(MX, 4, 3, lane, th2_mix<true, true, KST>(a.th1, H, lane));     // T1, accumulator operand
   }
-  const Th2Mix* mx = reinterpret_cast<const Th2Mix*>(MX) + lane;
+  auto mx = [&](int k) { return th2_mx_get(MX, 4, k, lane); };
   f32x16 adk[HPW][NT], adv[HPW][NT];
 #pragma unroll
   for (int e = 0; e < HPW; ++e)
@@ -867,8 +880,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
       f32x16 p[G], dp[G];
 #pragma unroll
       for (int u = 0; u < G; ++u) {
-        p[u] = th2_mix_img<KST>(XS, (b0 + u * NW) & 31, mx[0], lane);
-        dp[u] = th2_mix_img<KST>(XG, (b0 + u * NW) & 31, mx[2 * 64], lane);
+        p[u] = th2_mix_img<KST>(XS, (b0 + u * NW) & 31, mx(0), lane);
+        dp[u] = th2_mix_img<KST>(XG, (b0 + u * NW) & 31, mx(2), lane);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
@@ -892,8 +905,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
           }
         }
         if (blk < 32) {
-          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(p[u], mx[64]), H, lane);       // P2_h over S_h at this key
-          th2_put_block<NR>(XG, blk, th2_mix_acc<KST>(dp[u], mx[3 * 64]), H, lane);  // dS_h over dP2_h
+          th2_put_block<NR>(XS, blk, th2_mix_acc<KST>(p[u], mx(1)), H, lane);       // P2_h over S_h at this key
+          th2_put_block<NR>(XG, blk, th2_mix_acc<KST>(dp[u], mx(3)), H, lane);  // dS_h over dP2_h
         }
       }
     }
