@@ -648,6 +648,20 @@ static int g8_launch(const NtArgs& g, hipStream_t st) {
                                          : g8_launch_bm<EPI, BN, BK, NS, 256>(g, st);
 }
 
+// GELU forward at K < 768 (the epilogue's VALU work, which scales with the outputs, outweighs the
+// reduction): 256 x 128 tiles when they put fewer outputs on the busiest CU than 224 / 256 x 192 --
+// DeiT-S / CaiT-S FF Dense_0 (M 25,216 / 25,088 into 1,536): 5 rounds of 32 K outputs against 4 of
+// 43 K, 68.0 -> 63.8 us same box (profiles/r05ai_g8_bn128_ab.txt; the GELU' input gradient measured
+// level, so it keeps the 192-wide tiles)
+static bool g8_gelu_bn128(int M, int N, int K) {
+  if (K >= 768 || N % 128 || dev_knob("SAE_G8_NO_BN128")) return false;
+  const long long G = device_cus();
+  const int bm = g8_pick_bm(M, N, 192);
+  const long long c192 = (((long long)(M + bm - 1) / bm * ((N + 191) / 192) + G - 1) / G) * bm * 192;
+  const long long c128 = (((long long)(M + 255) / 256 * (N / 128) + G - 1) / G) * 256 * 128;
+  return c128 < c192;
+}
+
 // one gemm8x launch (BM x BN tiles, ping-pong wave groups, one tile per workgroup)
 template <int EPI, int BN, int BM>
 static int g8x_launch_bm(const NtArgs& g, hipStream_t st) {
@@ -1361,6 +1375,10 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
       && !dev_knob("SAE_NT_NO_G8")
 #endif
   ) {
+    if (epilogue == SAE_EPI_GELU && g8_gelu_bn128(M, N, K)) {
+      if (int rc = g8_launch_bm<kEpiGelu, 128, 64, 2, 256>(g, st)) return rc;
+      return check_launch("gemm8_nt");
+    }
     const int rc = epilogue == SAE_EPI_NONE   ? g8_launch<kEpiNone, 192, 64, 2>(g, st)
                    : epilogue == SAE_EPI_GELU ? g8_launch<kEpiGelu, 192, 64, 2>(g, st)
                                               : g8_launch<kEpiDGelu, 192, 64, 2>(g, st);
