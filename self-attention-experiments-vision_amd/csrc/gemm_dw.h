@@ -273,25 +273,8 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce_kernel(DwArgs a) {
       const long long e = base + col;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if (e < n4 && s0 < s1) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.part) + e;
-        const long long st4 = stride / 4;
-        acc = src[s0 * st4];
-        int s = s0 + 1;
-        // four loads in flight, added in split order (the same sum as one at a time)
-        for (; s + 4 <= s1; s += 4) {
-          const f32x4 v0 = src[s * st4], v1 = src[(s + 1) * st4], v2 = src[(s + 2) * st4], v3 = src[(s + 3) * st4];
-          acc += v0;
-          acc += v1;
-          acc += v2;
-          acc += v3;
-        }
-        if (s + 2 <= s1) {
-          const f32x4 v0 = src[s * st4], v1 = src[(s + 1) * st4];
-          acc += v0;
-          acc += v1;
-          s += 2;
-        }
-        if (s < s1) acc += src[s * st4];
+        acc = *reinterpret_cast<const f32x4*>(a.part + s0 * stride + 4 * e);
+        for (int s = s0 + 1; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(a.part + s * stride + 4 * e);
       }
       red[grp][col] = acc;
       __syncthreads();
