@@ -215,7 +215,7 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
 #define SAE_NT_ROUTE_NONE 0           /* shape not supported: sae_gemm_nt returns SAE_EUNSUPPORTED */
 #define SAE_NT_ROUTE_TILE128 1        /* 128-row tiles (gemm_nt_kernel), K % 64 == 0 */
 #define SAE_NT_ROUTE_TILE128_KTAIL 2  /* 128-row tiles, K % 8 == 0 with a partial last K stage */
-#define SAE_NT_ROUTE_GEMM8 3          /* persistent 224/256 x 192 tiles, LDS-DMA (gemm8_nt_kernel) */
+#define SAE_NT_ROUTE_GEMM8 3          /* persistent 224/256 x 192 tiles (GELU forward at K < 768: 256 x 128 where that loads the CUs more evenly), LDS-DMA (gemm8_nt_kernel) */
 #define SAE_NT_ROUTE_GEMM8X 4         /* ping-pong 256 x 256 tiles, LDS-DMA (gemm8x_nt_kernel) */
 int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue);
 /* The same projections at compute dtype float32 (the reference's fp32 trunks, cait.py:147-154,
