@@ -456,7 +456,7 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
 // two heads per wave (eight waves of <= 256 registers; sixteen waves of 128 spilled heavily).
 template <int DP, int NWMAX, bool ROT, int HPW, bool LEAN = false> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32, nw = (a.H + HPW - 1) / HPW;
-  const size_t lds = th2_lds_bytes<DP, NWMAX * HPW <= 8>(a.H);
+  const size_t lds = th2_lds_bytes<DP, NWMAX * HPW <= 8>(a.H, 1, LEAN);
   if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>, lds)) return rc;
   hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   return check_launch("th2_fwd");

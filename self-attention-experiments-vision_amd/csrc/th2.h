@@ -290,8 +290,22 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
     }
   // S1 = T1^T S with T1 scaled by log2 e: the mixed logits come out in the log2 domain, so the
   // statistics and probabilities need no per-element scaling
-  const Th2Mix m1 = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);
-  const Th2Mix m2 = th2_mix<false, true, KST>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
+  // LEAN (128 registers): the two operands live in an LDS table written by wave 0 before the first
+  // barrier and are re-read per use (held in registers they were spilled to scratch and reloaded in
+  // the output sweep)
+  Th2Mix m1r, m2r;
+  char* const mxt = smem + 2 * IMG + H * I::bytes(32);
+  if constexpr (LEAN) {
+    if (w == 0) {
+      th2_mx_put(mxt, 2, 0, lane, th2_mix<false, false, KST>(a.th1, H, lane, kLog2e));
+      th2_mx_put(mxt, 2, 1, lane, th2_mix<false, true, KST>(a.th2, H, lane));
+    }
+  } else {
+    m1r = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);
+    m2r = th2_mix<false, true, KST>(a.th2, H, lane);    // P2 = T2^T P (accumulator operand)
+  }
+  auto m1 = [&]() -> Th2Mix { if constexpr (LEAN) return th2_mx_get(mxt, 2, 0, lane); else return m1r; };
+  auto m2 = [&]() -> Th2Mix { if constexpr (LEAN) return th2_mx_get(mxt, 2, 1, lane); else return m2r; };
   const int nkt = (a.Nk + 31) / 32;
 
   // ---- pass 0: row statistics (log2 domain) of the mixed logits, per (head i, query) in this
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
       for (int u = 0; u < SG; ++u) {   // independent chains: issued together, blocks past the end clamped
         const int blk = b0 + u * NW;
         ok[u] = blk < 32 && kt * 32 + blk < a.Nk;
-        c[u] = th2_mix_img<KST>(xs, blk & 31, m1, lane);
+        c[u] = th2_mix_img<KST>(xs, blk & 31, m1(), lane);
       }
       if (!ok[0]) break;   // (the later blocks of the group lie further out)
 #pragma unroll
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
     for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 c[G];
 #pragma unroll
-      for (int u = 0; u < G; ++u) c[u] = th2_mix_img<KST>(xs, (b0 + u * NW) & 31, m1, lane);
+      for (int u = 0; u < G; ++u) c[u] = th2_mix_img<KST>(xs, (b0 + u * NW) & 31, m1(), lane);
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int blk = b0 + u * NW;
@@ -416,7 +430,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
 #pragma unroll
           for (int r = 8; r < 16; ++r) c[u][r] = 0.f;
         }
-        c[u] = th2_mix_acc<KST>(c[u], m2);
+        c[u] = th2_mix_acc<KST>(c[u], m2());
       }
 #pragma unroll
       for (int u = 0; u < G; ++u)
@@ -969,8 +983,10 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
 
 // LDS: two exchange images + per-head 32-row staging (two per head in th2_bwd_kv at <= 8 waves);
 // th2_bwd_q with two heads per wave adds its mix-operand table (3 x 64 lanes x 32 bytes)
-template <int DP, bool KST> constexpr size_t th2_lds_bytes(int H, int hpw = 1) {
-  return 2 * (size_t)th2_img<KST>() + (size_t)H * Img<__bf16, DP>::bytes(32) + (hpw > 1 ? 3 * 64 * 32 : 0);
+// (th2_fwd LEAN: its two mix operands, 2 x 64 lanes x 32 bytes)
+template <int DP, bool KST> constexpr size_t th2_lds_bytes(int H, int hpw = 1, bool lean = false) {
+  return 2 * (size_t)th2_img<KST>() + (size_t)H * Img<__bf16, DP>::bytes(32) + (hpw > 1 ? 3 * 64 * 32 : 0) +
+         (lean ? 2 * 64 * 32 : 0);
 }
 
 template <int DP, bool KST> constexpr size_t th2_kv_lds_bytes(int H, bool two_buffers) {
