@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
     }
   };
   auto stats = [&](int kt) {   // this wave's blocks of tile kt, groups of SG: one max update each
-    constexpr int SG = LEAN ? 2 : 4;
+    constexpr int SG = 4;   // (LEAN too since its mix operands moved to LDS: no extra spills)
     const char* xs = XS;
     for (int b0 = w; b0 < 32; b0 += SG * NW) {
       f32x16 c[SG];
