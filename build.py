@@ -9,6 +9,7 @@ libsae_attn_stamp.so (the dev knobs plus in-kernel s_memtime stamps, tools/stamp
 libsae_attn.so never reads the environment on a launch path.
 """
 import argparse
+import hashlib
 import os
 import subprocess
 import sys
@@ -54,10 +55,8 @@ def unit_deps(path, seen=None):
 
 # translation units: (source, extra flags).  capi.hip keeps every MFMA accumulator in VGPRs
 # (-amdgpu-mfma-vgpr-form: the exp / rescale VALU reads them directly); bwd_agpr.hip holds the
-# one-wave-per-SIMD kernels, whose dK / dV accumulators go to the AGPR half of the register file;
-# attn5.hip / bwd5.hip the round-5 attention kernels (fwd5.h / bwd5.h).
-UNITS = [("capi.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd_agpr.hip", []),
-         ("attn5.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd5.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"])]
+# one-wave-per-SIMD kernels, whose dK / dV accumulators go to the AGPR half of the register file.
+UNITS = [("capi.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]), ("bwd_agpr.hip", [])]
 
 
 def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
@@ -75,9 +74,11 @@ def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
     if stamps:
         common.append("-DSAE_STAMPS")
     tag = os.path.basename(out).replace(".so", "") + ("_g" if debug else "")
-    # objects cached per library flavour: a unit is recompiled only when it or a header it
+    # objects cached per library flavour and compile command (compiler, arch, flags: a change of
+    # any of them is a different directory): a unit is recompiled only when it or a header it
     # includes changed (capi.hip takes ~2 minutes; the attention units seconds)
-    objdir = os.path.join(ROOT, "build", tag)
+    key = hashlib.sha1(repr((common, UNITS)).encode()).hexdigest()[:12]
+    objdir = os.path.join(ROOT, "build", f"{tag}_{ARCH}_{key}")
     os.makedirs(objdir, exist_ok=True)
     objs, procs = [], []
     for src, extra in UNITS:
@@ -91,10 +92,14 @@ def build(force=False, debug=False, verbose=True, dev=False, stamps=False):
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
         procs.append((subprocess.Popen(cmd), obj))
-    for p, obj in procs:
+    failed = None
+    for p, obj in procs:   # wait for every child before reporting a failure
         if p.wait() != 0:
-            raise subprocess.CalledProcessError(p.returncode, "hipcc")
-        os.replace(obj + ".tmp", obj)
+            failed = failed or p.returncode
+        else:
+            os.replace(obj + ".tmp", obj)
+    if failed is not None:
+        raise subprocess.CalledProcessError(failed, "hipcc")
     link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print("[build]", " ".join(link), flush=True)

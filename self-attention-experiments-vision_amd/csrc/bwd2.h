@@ -24,9 +24,7 @@ namespace sae {
 // (fwd2.h rel_onehot8 / rel_qrow8); the dQ pass also forms dbias^T = onehot^T dS^T on the matrix
 // pipe -- one more 32 x 32 accumulator, complete per query row because the pass sweeps every key
 // -- and stores dbias_h / dbias_w (deterministic, no atomics).
-// PUB2: publish the dK / dV pass's row constants ready to use (bwd5.h, the LDS-DMA staged pass):
-// -delta at delta[row] and lse * log2 e at delta[B H Nq + row]
-template <int DP, int NW, int MINW, bool ROT = false, bool REL = false, bool PUB2 = false>
+template <int DP, int NW, int MINW, bool ROT = false, bool REL = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = FF::NS, NT = FF::NT, TILE = FF::TILE;
@@ -88,14 +86,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_bwd2_dq_kernel(AttnArgs a)
     }
   }
   const bool qok = q < a.Nq;
-  if constexpr (PUB2) {
-    if (qok && h == 0) {
-      a.delta[rowoff + q] = -dlt;
-      a.delta[(size_t)a.B * a.H * a.Nq + rowoff + q] = a.lse[rowoff + q] * kLog2e;
-    }
-  } else {
-    if (qok && h == 0) a.delta[rowoff + q] = dlt;
-  }
+  if (qok && h == 0) a.delta[rowoff + q] = dlt;
   const float lsc2 = qok ? -a.lse[rowoff + q] * kLog2e : -kInf;
   const float sl2 = a.scale * kLog2e;
 

@@ -33,11 +33,6 @@
 
 using namespace sae;
 
-namespace sae {
-// round-5 attention launchers (attn5.hip): forward at head_dim <= 64, no rotary / relative logits
-hipError_t fwd5_launch(hipStream_t st, const AttnArgs& a, int variant);
-}  // namespace sae
-
 namespace {
 
 thread_local std::string g_err;
@@ -229,15 +224,6 @@ constexpr int dev_knob(const char*) { return 0; }
 #endif
 
 template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const AttnArgs& a, int var) {
-  if constexpr (DP == 64 && !ROT) {
-    // fwd5 (one basic block per full tile, pre-scaled queries, -max as the score MFMAs' initial
-    // accumulator); dev builds: SAE_FWD_VARIANT 20-23 select its forms
-    if (var >= 20 && var <= 25) {   // measured slower than fwd2 (profiles/r05b_attn_ab.txt): dev only
-      const hipError_t e = fwd5_launch(st, a, var - 20);
-      if (e != hipSuccess) return fail(SAE_EHIP, "attn_fwd5: launch failed: %s", hipGetErrorString(e));
-      return ok();
-    }
-  }
 #ifdef SAE_DEV_KNOBS
   if (!ROT) switch (var) {
     case 2: return fwd2_run<DP, 8, 2, true>(st, a);
@@ -300,45 +286,8 @@ template <int DP, bool ROT = false> int bwd2_run_default(hipStream_t st, const A
 namespace sae {
 hipError_t bwd2_dkdv_agpr(hipStream_t st, const AttnArgs& a, int dp, bool pipe);   // bwd_agpr.hip
 hipError_t bwd2_agpr128(hipStream_t st, const AttnArgs& a, bool rel, int variant);  // bwd_agpr.hip
-hipError_t bwd5_dkdv_launch(hipStream_t st, const AttnArgs& a, int variant);       // bwd5.hip
-hipError_t bwd6_dq_launch(hipStream_t st, const AttnArgs& a, int prio);             // bwd5.hip
-hipError_t bwd7_launch(hipStream_t st, const AttnArgs& a, int variant);             // bwd5.hip
 }
 namespace {
-
-// two-pass backward with the round-5 dK / dV pass (bwd5.h: both query halves of a tile in one
-// hand-ordered basic block)
-template <int DP> int bwd5_run(hipStream_t st, const AttnArgs& a, int variant) {
-  static_assert(DP == 64, "bwd5: head_dim <= 64");
-  if (variant == 15 || variant == 16) {   // LDS-DMA staged dK / dV (bwd7), 16: one wave per SIMD
-    const hipError_t e = bwd7_launch(st, a, variant == 16 ? 1 : 0);
-    if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd7: %s", hipGetErrorString(e));
-    return ok();
-  }
-  if (variant >= 8 && variant <= 10) {   // ping-pong dQ pass; 8: + ping-pong dK / dV, 9: + bwd2 dK / dV, 10: both at setprio
-    const hipError_t e = bwd6_dq_launch(st, a, variant == 10);
-    if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd6_dq: %s", hipGetErrorString(e));
-    if (variant == 9) {
-      const size_t lds = 2 * (2 * (size_t)F2<DP>::TILE + 512);
-      const long long grid = (long long)((a.Nk + 127) / 128) * a.H * a.B;
-      hipLaunchKernelGGL((attn_bwd2_dkdv_kernel<DP, 4, 2>), dim3((unsigned)grid), dim3(256), lds, st, a);
-      return check_launch("attn_bwd2_dkdv");
-    }
-    const hipError_t e2 = bwd5_dkdv_launch(st, a, variant == 10 ? 8 : 7);
-    if (e2 != hipSuccess) return fail(SAE_EHIP, "attn_bwd6_dkdv: %s", hipGetErrorString(e2));
-    return ok();
-  }
-  {
-    const long long grid = (long long)((a.Nq + 127) / 128) * a.H * a.B;
-    if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-    const size_t lds = 4 * (size_t)F2<DP>::TILE;
-    hipLaunchKernelGGL((attn_bwd2_dq_kernel<DP, 4, 2>), dim3((unsigned)grid), dim3(256), lds, st, a);
-    if (int rc = check_launch("attn_bwd2_dq")) return rc;
-  }
-  const hipError_t e = bwd5_dkdv_launch(st, a, variant);
-  if (e != hipSuccess) return fail(SAE_EHIP, "attn_bwd5_dkdv: %s", hipGetErrorString(e));
-  return ok();
-}
 
 // two-pass backward with the dK / dV pass from bwd_agpr.hip (one wave per SIMD, AGPR accumulators)
 template <int DP> int bwd2_run_agpr(hipStream_t st, const AttnArgs& a, bool pipe) {
@@ -816,7 +765,7 @@ static size_t delta_bytes(const sae_attn_desc* d) {
 
 size_t sae_attn_bwd_workspace_bytes(const sae_attn_desc* d) {
   if (!d) return 0;
-  return 2 * delta_bytes(d);   // delta [B, H, Nq] (+ lse * log2 e for the round-5 dK / dV pass)
+  return delta_bytes(d);   // delta [B, H, Nq]
 }
 
 static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, const void* k, const void* v,
@@ -903,9 +852,6 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
     }
 #ifdef SAE_DEV_KNOBS
     if (dp == 64 && (var == 10 || var == 11)) return bwd2_run_agpr<64>(st, a, var == 11);
-    // key ranges > 256 at head_dim <= 64 (ViT-B/16@384): the round-5 dK / dV pass; dev builds:
-    // SAE_BWD_VARIANT 19 = the round-4 bwd2 pair, 20-23 the bwd5 forms, 24-26 timing probes
-    if (dp == 64 && var >= 20 && var <= 39) return bwd5_run<64>(st, a, var - 20);
 #endif
     if (dp == 32) return bwd2_run_default<32>(st, a);
     if (dp == 64) return bwd2_run_default<64>(st, a);
@@ -1391,11 +1337,13 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
   // still gives >= 2 tiles per CU; 128 otherwise (plain GEMMs: no gain, profiles/r03n_nt_probe.txt)
   const long long tn = (N + kNtT - 1) / kNtT;
   const long long grid128 = (long long)((M + kNtT - 1) / kNtT) * tn;
+  // every launch below uses 128-row tiles (grid128) or taller ones (fewer workgroups)
+  if (grid128 >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "gemm_nt: grid too large");
   bool tall = epilogue != SAE_EPI_NONE && K >= 768 && (long long)((M + 255) / 256) * tn >= 512;
 #ifdef SAE_DEV_KNOBS
   const int ntv = dev_knob("SAE_NT_VARIANT");
   if (ntv) tall = ntv == 2;
-  if (ntv == 3 || ntv == 4) {   // LDS-DMA staging, 3 / 4 stage buffers
+  if ((ntv == 3 || ntv == 4) && K % kNtK == 0) {   // LDS-DMA staging, 3 / 4 stage buffers (no K tail)
     int rc;
     if (ntv == 3)
       rc = epilogue == SAE_EPI_NONE ? nt_launch<kEpiNone, NtDmaA<3>>(g, grid128, st)
@@ -1411,7 +1359,6 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
 #endif
   const int TM = tall ? 256 : kNtT;
   const long long grid = (long long)((M + TM - 1) / TM) * tn;
-  if (grid >= (1LL << 31)) return fail(SAE_EUNSUPPORTED, "gemm_nt: grid too large");
   // stage depth: the GELU / GELU' epilogue GEMMs at reduction depth <= 384 (DeiT-S / CaiT FF
   // block) run 32-deep stages (32 KiB of LDS: 3-4 workgroups per CU, so one tile's epilogue VALU
   // overlaps other tiles' MFMAs; same-box step A/B 9.19 -> 9.10 ms); deeper reductions (ViT-B,

@@ -880,15 +880,17 @@ class _Dense(torch.autograd.Function):
             return _Dense._backward_f32(ctx, x2, wd, dy2)
         if use_gemm_nt(J, I) and _nt_ok(dy2, I) and wd.dtype == torch.bfloat16:
             dx = gemm_nt(dy2, wd).view(ctx.xshape).to(ctx.xdtype)
-        elif (wd.dtype == torch.bfloat16 and wt is not None and dy2.shape[0] % 8 == 0 and _dw_ok(dy2, wt)):
-            # K = J not a multiple of 8 (a classifier head with e.g. 10 classes) -- the reduction
-            # runs over the ROWS of dY^T [J, M] and W^T [J, I], i.e. on the weight-gradient kernel:
-            # dx[m][i] = sum_j dY^T[j][m] W^T[j][i], fp32 then the activation dtype
-            dxf = torch.empty((dy2.shape[0], I), dtype=torch.float32, device=dy2.device)
-            gemm_dw(dy2.t().contiguous(), wt, dxf)
-            dx = dxf.view(ctx.xshape).to(ctx.xdtype)
         else:
-            dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
+            dyt = dy2.t().contiguous() if (wd.dtype == torch.bfloat16 and wt is not None) else None
+            if dyt is not None and _dw_ok(dyt, wt):
+                # K = J not a multiple of 8 (a classifier head with e.g. 10 classes) -- the reduction
+                # runs over the ROWS of dY^T [J, M] and W^T [J, I], i.e. on the weight-gradient
+                # kernel: dx[m][i] = sum_j dY^T[j][m] W^T[j][i], fp32 then the activation dtype
+                dxf = torch.empty((dy2.shape[0], I), dtype=torch.float32, device=dy2.device)
+                gemm_dw(dyt, wt, dxf)
+                dx = dxf.view(ctx.xshape).to(ctx.xdtype)
+            else:
+                dx = (dy2 @ wd.t()).view(ctx.xshape).to(ctx.xdtype)
         widths = [n for n, _ in ctx.wmeta]
         blocked = len(widths) > 1 and len(set(widths)) == 1 and widths[0] % 4 == 0
         sw, sb = ctx.sinks_w, ctx.sink_b

@@ -33,17 +33,29 @@ def rel_err(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def _ff_epilogues():
+    # the epilogue codes the FF block actually passes (ops.py: FF_GELU_GRAD on by default saves
+    # gelu'(h) in Dense_0's forward and multiplies by it in Dense_1's input gradient)
+    import sae_vision_amd.ops as ops
+    if ops.FF_GELU_GRAD:
+        return ops.EPI_GELU_GRAD, ops.EPI_MUL_AUX
+    return ops.EPI_GELU, ops.EPI_DGELU
+
+
 def _block_gemms(M, C, hidden):
     # (K, N, epilogue) of the forward / input-gradient GEMMs of one encoder block
+    e_fwd, e_dx = _ff_epilogues()
     return {"qkv_fwd": (C, 3 * C, 0), "qkv_dx": (3 * C, C, 0), "oproj_fwd": (C, C, 0), "oproj_dx": (C, C, 0),
-            "ff0_fwd": (C, hidden, 1), "ff0_dx": (hidden, C, 0), "ff1_fwd": (hidden, C, 0),
-            "ff1_dx": (C, hidden, 2)}
+            "ff0_fwd": (C, hidden, e_fwd), "ff0_dx": (hidden, C, 0), "ff1_fwd": (hidden, C, 0),
+            "ff1_dx": (C, hidden, e_dx)}
 
 
 @pytest.mark.parametrize("name,B,img,C,H,expect", [
-    ("deit_s_width", 24, 224, 384, 6, {k: GEMM8 for k in _block_gemms(0, 384, 1536)}),
+    ("deit_s_width", 24, 224, 384, 6, {k: GEMM8 for k in ("qkv_fwd", "qkv_dx", "oproj_fwd", "oproj_dx", "ff0_fwd",
+                                                           "ff0_dx", "ff1_fwd", "ff1_dx")}),
     ("vit_b384_width", 8, 384, 768, 12, {"qkv_fwd": GEMM8, "ff0_fwd": GEMM8, "qkv_dx": GEMM8X, "oproj_fwd": GEMM8X,
-                                         "oproj_dx": GEMM8X, "ff0_dx": GEMM8X, "ff1_fwd": GEMM8X}),
+                                         "oproj_dx": GEMM8X, "ff0_dx": GEMM8X, "ff1_fwd": GEMM8X,
+                                         "ff1_dx": GEMM8}),
 ])
 def test_train_step_production_rows_vs_oracle(dev, name, B, img, C, H, expect):
     import torch
