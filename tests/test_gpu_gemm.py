@@ -108,6 +108,34 @@ def test_classifier_head_dense(dev, rows, C):
     assert float((w.grad.double() - ref_w).abs().max() / ref_w.abs().max()) <= 1e-5
 
 
+@pytest.mark.parametrize("rows,C,J", [(16, 192, 10), (128, 384, 10), (24, 768, 37)])
+def test_small_head_dgrad_on_gemm_dw(dev, monkeypatch, rows, C, J):
+    """A small-M classifier head whose class count J is not a multiple of 8 (e.g. 10 classes): the
+    input gradient dX = dY W^T reduces over J, so it runs on the weight-gradient kernel over the
+    ROWS of dY^T [J, M] and the bf16 W^T [J, C] the forward saved (ops.py _Dense.backward); the
+    test asserts that route is taken (not the library GEMM) and checks dX against float64."""
+    import sae_vision_amd.ops as ops
+    calls = []
+    real = ops.gemm_dw
+
+    def spy(x2, dy2, dw, *a, **k):
+        calls.append((tuple(x2.shape), tuple(dy2.shape), tuple(dw.shape)))
+        return real(x2, dy2, dw, *a, **k)
+
+    monkeypatch.setattr(ops, "gemm_dw", spy)
+    g = torch.Generator(device=dev).manual_seed(rows + J)
+    x = torch.randn(rows, C, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(C, J, device=dev, generator=g) * 0.05).requires_grad_()
+    b = torch.randn(J, device=dev, generator=g).requires_grad_()
+    dy = torch.randn(rows, J, device=dev, generator=g).to(torch.bfloat16)
+    y = ops.dense(x, w, b, torch.bfloat16)
+    y.backward(dy)
+    assert ((J, rows), (J, C), (rows, C)) in calls, calls   # dX = (dY^T)^T W^T on sae_gemm_dw
+    wd = w.detach().to(torch.bfloat16).double()
+    ref_x = dy.double() @ wd.t()
+    assert float((x.grad.double() - ref_x).abs().max() / ref_x.abs().max()) <= 2e-2
+
+
 def test_gemm_dw_blocked_layout(dev):
     """sae_gemm_dw_blocked: dW in contiguous column blocks [J/jb, I, jb] equals the plain layout."""
     import sae_vision_amd.ops as ops
