@@ -289,7 +289,14 @@ def main():
     ap.add_argument("--no-persistent-casts", action="store_true",
                     help="cast every Dense kernel to bf16 at the start of each forward instead of the optimizer "
                          "writing the bf16 copies in its update")
+    ap.add_argument("--emulate-rccl", default="",
+                    help="CHANNELS,BUSBW_GBPS,WORLD: one-GPU contention emulation of a WORLD-GPU node -- beside "
+                         "each bucket's all-reduce, CHANNELS workgroups hold CUs for the bucket's ring time at "
+                         "BUSBW_GBPS (implies --world1-rccl; a diagnostic, never the bench line)")
     args = ap.parse_args()
+    if args.emulate_rccl:
+        os.environ["SAE_EMULATE_RCCL"] = args.emulate_rccl
+        args.world1_rccl = True
     if args.world1_rccl:
         os.environ["SAE_WORLD1_RCCL"] = "1"
     # stdout carries exactly ONE line, the JSON result: everything else written to fd 1 by the
@@ -417,6 +424,7 @@ def main():
                    # what actually ran: a capture that failed leaves the step eager (train.py)
                    "step": step_label(step, use_graph),
                    "collective": {"mode": step.collective, "process_group": dist.get_backend() if step.pg else None,
+                                  "emulated_rccl": args.emulate_rccl or None,
                                   "buckets": len(getattr(step, "_buckets", [])), "bucket_cap_mb": args.bucket_mb}},
         "host_submit_ms_per_step": round(host / args.steps * 1e3, 3),
         "roofline": roof,

@@ -395,6 +395,13 @@ int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void*
                         int32_t dtype, const int64_t* labels, float alpha, const float* lse,
                         const float* grad_loss, void* dlogits, int64_t ldd);
 
+/* Diagnostic: occupy `workgroups` workgroups of `threads` threads, each holding `lds_bytes` of LDS,
+   for `usec` microseconds (a timed s_sleep loop, no memory traffic), on `stream`.  Used by
+   bench.py --emulate-rccl to stand in, on one GPU, for the RCCL all-reduce kernels that share the
+   CUs with the backward on an 8-GPU node (one workgroup per ring channel, busy for the bucket's
+   ring time).  threads in [64, 1024], lds_bytes <= 160 KiB. */
+int sae_occupy_cus(void* stream, int32_t workgroups, int32_t threads, int32_t lds_bytes, float usec);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);
 

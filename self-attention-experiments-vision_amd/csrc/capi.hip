@@ -10,6 +10,7 @@
 #include <string>
 #include <algorithm>
 #include <type_traits>
+#include <mutex>
 
 #include "../../include/sae_attn.h"
 #include "attn_kernels.h"
@@ -170,15 +171,15 @@ template <typename T, int DP, bool VEC, bool REL> struct FwdL {
 
 // lean bf16 forward (fwd2.h): NW waves x 32 query rows per workgroup
 template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false,
-          bool FIX = false>
+          bool FIX = false, bool PSC = false>
 int fwd2_run(hipStream_t st, const AttnArgs& a) {
   const int nqb = (a.Nq + 32 * NW - 1) / (32 * NW);
   const long long grid = (long long)nqb * a.H * a.B;
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
   const size_t lds = 4 * (size_t)F2<DP>::TILE + (REL ? 2 * kRelImg : 0);
-  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX>, lds)) return rc;
-  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX>), dim3((unsigned)grid), dim3(64 * NW),
-                     lds, st, a);
+  if (int rc = lds_attr((const void*)attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX, PSC>, lds)) return rc;
+  hipLaunchKernelGGL((attn_fwd2_kernel<DP, NW, MINW, LSUM, ROT, NSU, REL, FIX, PSC>), dim3((unsigned)grid),
+                     dim3(64 * NW), lds, st, a);
   return check_launch("attn_fwd2");
 }
 
@@ -234,6 +235,11 @@ template <int DP, bool ROT = false> int fwd2_dispatch(hipStream_t st, const Attn
     case 8: return fwd2_run<DP, 4, 2, true, false, DP / 16, false, true>(st, a);
     case 9: return fwd2_run<DP, 4, 3, false, false, DP / 16, false, true>(st, a);
     default: break;
+  }
+  if constexpr (DP <= 64) {
+    if (!ROT && var == 40) return fwd2_run<DP, 4, 3, false, false, DP / 16, false, true, true>(st, a);   // prescaled q
+    if (!ROT && var == 41) return fwd2_run<DP, 4, 3, true, false, DP / 16, false, true, true>(st, a);    // + MFMA row sum
+    if (!ROT && var == 42) return fwd2_run<DP, 4, 2, false, false, DP / 16, false, true, true>(st, a);
   }
 #endif
   // D <= 64 without rotary: three waves per SIMD, row sum on the VALU, running max fixed by the
@@ -581,13 +587,55 @@ static int g8_pick_bm(int M, int N, int BN) {
   return cost(224) < cost(256) ? 224 : 256;
 }
 
-// one persistent gemm8 launch (BM x BN tiles, one 8-wave workgroup per CU)
+// Work-stealing counters of the persistent gemm8 launches (gemm8.h, DYN; dev builds): 8 group tickets
+// and a done word per slot, each on a 128-byte line of its own; a slot belongs to one stream (launches on one
+// stream are ordered, so a slot is never used by two running launches; the last workgroup of a
+// launch resets it).  A graph captured on a stream keeps that stream's slot in its kernel nodes.
+#ifdef SAE_DEV_KNOBS
+constexpr int kG8Slots = 64, kG8SlotWords = 288;   // 8 group tickets + done, 128 bytes apart
+__device__ unsigned g_g8_ctr[kG8Slots * kG8SlotWords];
+
+static unsigned* g8_slot(hipStream_t st) {
+  static std::mutex mu;
+  static hipStream_t owner[64][kG8Slots];
+  static int used[64] = {0};
+  static unsigned* base[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_g8_ctr)) != hipSuccess) return nullptr;
+    base[dev] = reinterpret_cast<unsigned*>(p);
+  }
+  for (int i = 0; i < used[dev]; ++i)
+    if (owner[dev][i] == st) return base[dev] + kG8SlotWords * i;
+  if (used[dev] == kG8Slots) return nullptr;   // more streams than slots: the static walk
+  owner[dev][used[dev]] = st;
+  return base[dev] + kG8SlotWords * used[dev]++;
+}
+#endif
+
+// one persistent gemm8 launch (BM x BN tiles, one 8-wave workgroup per CU).  The work-stealing walk
+// (DYN, dev builds: SAE_G8_DYN=1) measured 3 % slower on the DeiT-S step and no better under the
+// one-GPU RCCL contention emulation (profiles/r06c_g8_dyn_ab.txt), so the release walk is static.
 template <int EPI, int BN, int BK, int NS, int BM>
-static int g8_launch_bm(const NtArgs& g, hipStream_t st) {
-  constexpr int lds = g8_lds_bytes<BN, BK, NS>();
-  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>, lds)) return rc;
-  const long long tiles = (long long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
+  constexpr int lds = g8_lds_bytes<BN, BK, NS>() + kG8TickBytes;
+  const long long tiles = (long long)((g0.M + BM - 1) / BM) * ((g0.N + BN - 1) / BN);
   const long long grid = std::min<long long>(tiles, device_cus());
+  NtArgs g = g0;
+#ifdef SAE_DEV_KNOBS
+  g.ctr = (NS == 2 && tiles > grid && grid >= 8 && dev_knob("SAE_G8_DYN")) ? g8_slot(st) : nullptr;
+  if (g.ctr) {
+    if constexpr (NS == 2) {
+      if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, true>, lds)) return rc;
+      hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, true>), dim3((unsigned)grid), dim3(512), lds, st, g);
+      return 0;
+    }
+  }
+#endif
+  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>, lds)) return rc;
   hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>), dim3((unsigned)grid), dim3(512), lds, st, g);
   return 0;
 }
@@ -1259,6 +1307,25 @@ int sae_gemm_f32(void* stream, int32_t M, int32_t N, int32_t K, const float* a, 
 }
 
 // ------------------------------------------------------------ forward / input-gradient GEMMs
+// bench.py --emulate-rccl: workgroups that hold their CU's slots (waves, LDS) for `ticks` of the
+// 100 MHz real-time counter while sleeping -- the CU footprint of an RCCL ring channel
+__global__ void occupy_cus_kernel(long long ticks) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) lds[0] = 0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+int sae_occupy_cus(void* stream, int32_t workgroups, int32_t threads, int32_t lds_bytes, float usec) {
+  if (workgroups < 1 || threads < 64 || threads > 1024 || lds_bytes < 0 || lds_bytes > 160 * 1024 || !(usec >= 0.f))
+    return fail(SAE_EINVAL, "occupy_cus: bad arguments (%d workgroups, %d threads, %d B LDS, %g us)", workgroups,
+                threads, lds_bytes, (double)usec);
+  if (int rc = lds_attr((const void*)occupy_cus_kernel, (size_t)lds_bytes)) return rc;
+  hipLaunchKernelGGL(occupy_cus_kernel, dim3((unsigned)workgroups), dim3((unsigned)threads), (size_t)lds_bytes,
+                     (hipStream_t)stream, (long long)(usec * 100.f));
+  return check_launch("occupy_cus");
+}
+
 int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue) {
   if (M < 1 || N < 1 || K < 1 || K % 8 || N % 8 || epilogue < SAE_EPI_NONE || epilogue > SAE_EPI_MUL_AUX)
     return SAE_NT_ROUTE_NONE;

@@ -146,16 +146,29 @@ struct F2Stage {
 // row's sum left [1, 2^64) (a later tile's score more than 64 log2 units above the first tile's
 // max).  P is fed to the MFMA in bf16, whose relative precision does not depend on magnitude,
 // so the result is that of the tracking sweep up to fp32 summation order.
-template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS, bool REL = false, bool FIX = false>
+// PSC: the query fragments arrive pre-scaled by scale * log2 e (bf16), so the scores come out of
+// the MFMA in the log2 domain; with FIX the score chains of every tile after the first start from
+// C = -m (the fixed running max, `cneg`), so the exponent is the accumulator itself: no per-score
+// FMA on the VALU (the tile's largest VALU item after exp).
+template <int DP, int NW, bool LSUM, bool FIRST, int NSU = F2<DP>::NS, bool REL = false, bool FIX = false,
+          bool PSC = false>
 __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, const bf16x8* qf, f32x16* acco,
                                           f32x16& lacc, float& m, float& l, int nvalid, float sl2,
                                           const unsigned* ka, const unsigned* va, int h,
                                           const char* ldsR = nullptr, const unsigned* ra = nullptr,
-                                          const bf16x8* qa = nullptr) {
+                                          const bf16x8* qa = nullptr, const f32x16* cneg = nullptr) {
   constexpr int NS = NSU, NT = F2<DP>::NT;
+  constexpr bool CIN = PSC && FIX && !FIRST;   // chains start from -m: s0 / s1 are exponents
   // nvalid: keys of this tile that exist (64 for every tile but the tail)
   const bool two = nvalid > 32;
-  f32x16 s0 = zero16(), s1 = zero16();
+  f32x16 s0, s1;
+  if constexpr (CIN) {
+    s0 = *cneg;
+    s1 = *cneg;
+  } else {
+    s0 = zero16();
+    s1 = zero16();
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ldsK + ka[s]);
@@ -194,7 +207,7 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
   }
-  mx = xhalf_max(mx) * sl2;
+  mx = PSC ? xhalf_max(mx) : xhalf_max(mx) * sl2;
   if constexpr (FIRST) {   // first tile: nothing accumulated yet, the running max starts here
     m = mx;
   } else if (!__all(mx - m <= 8.f)) {
@@ -213,11 +226,27 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
     }
   }
   }
+  if constexpr (CIN) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) s0[r] = ex2(__builtin_fmaf(s0[r], sl2, -m));
-  if (two) {
+    for (int r = 0; r < 16; ++r) s0[r] = ex2(s0[r]);
+    if (two) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s1[r] = ex2(__builtin_fmaf(s1[r], sl2, -m));
+      for (int r = 0; r < 16; ++r) s1[r] = ex2(s1[r]);
+    }
+  } else if constexpr (PSC) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s0[r] = ex2(s0[r] - m);
+    if (two) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s1[r] = ex2(s1[r] - m);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s0[r] = ex2(__builtin_fmaf(s0[r], sl2, -m));
+    if (two) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s1[r] = ex2(__builtin_fmaf(s1[r], sl2, -m));
+    }
   }
   if constexpr (!LSUM) {
     // pairwise (depth 4 per half): a serial chain of 32 dependent adds sat on the tile's critical
@@ -269,7 +298,7 @@ __device__ __forceinline__ void fwd2_tile(const char* ldsK, const char* ldsV, co
 // REL: BoTNet relative logits as two extra score k-steps (rel_onehot8 / rel_qrow8 above); the
 // one-hot images follow the K / V buffers in LDS.
 template <int DP, int NW, int MINW, bool LSUM, bool ROT = false, int NSU = DP / 16, bool REL = false,
-          bool FIX = false>
+          bool FIX = false, bool PSC = false>
 __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   using FF = F2<DP>;
   constexpr int NS = NSU, NT = FF::NT, TILE = FF::TILE;
@@ -317,6 +346,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) qf[s] = rope8<1>(qf[s], a.rope, q, 16 * s + 8 * h);
     }
+    if constexpr (PSC) {   // q * scale * log2 e, rounded to bf16 (the scores come out in log2 units)
+      const float c = a.scale * kLog2e;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * c);
+    }
   }
   // REL: query-bias fragments (columns 16s + 8h .. + 7) and the one-hot row reads
   bf16x8 qa[2];
@@ -347,6 +383,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
   }
 
   f32x16 acco[NT], lacc;   // written first by the peeled first tile (zero C operand)
+  f32x16 cneg;             // PSC + FIX: -m, the C operand of every later tile's score chains
   float m = -kInf, l = 0.f;
   const float sl2 = a.scale * kLog2e;
 
@@ -368,10 +405,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void attn_fwd2_kernel(AttnArgs a) {
       kst.load(rk, (unsigned)(t + 1) * kstep);
       vst.load(rv, (unsigned)(t + 1) * vstep);
     }
-    if constexpr (decltype(compute_c)::value)
-      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU, REL, decltype(fix_c)::value>(cur, cur + TILE, qf, acco, lacc, m, l,
-                                                             min(64, a.Nk - 64 * t), sl2, ka, va, h,
-                                                             rimg + bsel * kRelImg, ra, qa);
+    if constexpr (decltype(compute_c)::value) {
+      fwd2_tile<DP, NW, LSUM, decltype(first_c)::value, NSU, REL, decltype(fix_c)::value, PSC>(
+          cur, cur + TILE, qf, acco, lacc, m, l, min(64, a.Nk - 64 * t), sl2, ka, va, h, rimg + bsel * kRelImg, ra,
+          qa, &cneg);
+      if constexpr (PSC && decltype(first_c)::value) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cneg[r] = -m;
+      }
+    }
     if (t + 1 < nkt) {
       if constexpr (ROT) kst.rope(a.rope, 64 * (t + 1), tid);
       kst.write(nxt);

@@ -97,6 +97,7 @@ template <int BN> constexpr int g8_scratch_bytes() { return 32 * (BN / 4 * 2 + 1
 template <int BN, int BK, int NS> constexpr int g8_lds_bytes() {
   return g8_ring_bytes<BN, BK, NS>() + 8 * g8_scratch_bytes<BN>();
 }
+constexpr int kG8TickBytes = 16;   // the DYN ticket word after the scratch images
 
 // Persistent: workgroup b walks tiles xcd_remap(b) + i G (G = gridDim.x <= #tiles; consecutive
 // logical tiles -- the N tiles of one 256-row block -- run on one XCD at the same time, so the A
@@ -104,9 +105,25 @@ template <int BN, int BK, int NS> constexpr int g8_lds_bytes() {
 // NS - 1 stages are in flight while a tile's epilogue drains its accumulators (through the
 // per-wave scratch, 32 rows at a time: 16-byte row-segment stores), so neither the prologue's load
 // latency nor the epilogue's stores stall the ring.
+// DYN (launches with more tiles than workgroups): work stealing.  The tiles are dealt to the 8
+// placement groups of the static walk (group x = hardware blocks b with b % 8 = x, which the
+// dispatcher puts on one XCD; xcd_remap gives group x the logical range R_x, and with it the tiles
+// R_x + i G), and each group's tiles are handed out in that order by a ticket counter of the group,
+// t(k) = R_x.start + k % |R_x| + (k / |R_x|) G -- the first tile of a workgroup too: a workgroup that
+// starts late (its CU held by an RCCL all-reduce kernel on the communication stream) finds its
+// group's tiles taken and leaves at once, where the static walk would hold the kernel's end back by
+// its whole tile list.  Wave 0 draws the ticket (one returning atomic) of the tile after the one the
+// issue cursor enters, a whole tile ahead, keeps it in an LDS word, and every wave reads it when the
+// cursor crosses the next tile boundary; the atomic is issued after a stage's DMA pieces and is
+// covered by the next stage's vmcnt(0) wait (NS = 2).  Each workgroup that draws a ticket past its
+// group's tiles adds to the slot's done counter; the last of the G resets the slot for the next
+// launch (capi.hip g8_slot: one slot per stream).  Every tile is computed the same way whoever takes
+// it: results are bit-identical to the static walk (tools/g8_dyn_check.py).  Placement only decides
+// speed: every group has workgroups (G >= 8), and each drains its own counter.
 // MODE (probe builds only): 0 = the kernel; 1 = no global stores; 2 = no MFMAs (staging only)
-template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256>
+template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256, bool DYN = false>
 __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
+  static_assert(!DYN || NS == 2, "dynamic walk: the ticket atomic rides on the vmcnt(0) stage waits of NS = 2");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using C = G8Cfg<BN, BM>;
   constexpr int RB = BK * 2;                  // image row bytes
@@ -124,9 +141,19 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   const int ntiles = ((a.M + BM - 1) / BM) * tn;
   const int G = gridDim.x;
   const int b0 = xcd_remap(blockIdx.x, G);
-  const int myt = (ntiles - b0 + G - 1) / G;  // tiles of this workgroup: b0, b0 + G, ...
+  // static: tiles b0, b0 + G, ...; DYN: one ticket of the placement group per tile
+  const int myt = DYN ? 0x3fffffff : (ntiles - b0 + G - 1) / G;
   const int nst = a.K / BK;
-  const int total = myt * nst;                // stages of this workgroup's stream
+  int total = DYN ? 0x7fffffff : myt * nst;   // stages of this workgroup's stream (DYN: found at the end)
+  volatile unsigned* tick = reinterpret_cast<volatile unsigned*>(smem + g8_lds_bytes<BN, BK, NS>());
+  unsigned tkv = 0;                           // wave 0: the returning ticket atomic in flight
+  int tile_e = b0, tile_o = b0;               // DYN: tile ids of the even / odd local tiles
+  auto tile_of = [&](int it) { return __builtin_amdgcn_readfirstlane((it & 1) ? tile_o : tile_e); };
+  // DYN: this workgroup's placement group and the group's logical range R_x (xcd_remap's blocks)
+  const int grp_x = blockIdx.x & 7, gq = G >> 3, gr = G & 7;
+  const int r_cnt = gq + (grp_x < gr), r_start = grp_x < gr ? grp_x * (gq + 1) : gr * (gq + 1) + (grp_x - gr) * gq;
+  unsigned* gctr = DYN ? a.ctr + 32 * grp_x : nullptr;   // the group's counter (its own 128-byte line)
+  auto ticket_tile = [&](unsigned k) { return r_start + (int)(k % (unsigned)r_cnt) + (int)(k / (unsigned)r_cnt) * G; };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -153,10 +180,16 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   int iti = 0, ist = 0, ibuf = 0;
   g8_u32x4 ra, rb;
   auto set_issue_tile = [&](int it) {
-    const int t = b0 + it * G;
+    const int t = DYN ? tile_of(it) : b0 + it * G;
     const int m0 = (t / tn) * BM, n0 = (t % tn) * BN;
     ra = g8_rsrc(a.a + (long long)m0 * a.lda, min(BM, a.M - m0), a.lda);
     rb = g8_rsrc(a.bt + (long long)n0 * a.ldb, min(BN, a.N - n0), a.ldb);
+  };
+  // DYN: wave 0 draws the ticket of the tile after the one the issue cursor is entering
+  auto draw_ticket = [&]() {
+    if (w == 0) {
+      if (lane == 0) tkv = __hip_atomic_fetch_add(gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   };
   auto issue_next = [&]() {
     const unsigned ko = (unsigned)ist * RB;
@@ -175,7 +208,30 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
     ibuf = ibuf + 1 == NS ? 0 : ibuf + 1;
     if (++ist == nst) {
       ist = 0;
-      if (++iti < myt) set_issue_tile(iti);
+      if constexpr (DYN) {
+        const int t = __builtin_amdgcn_readfirstlane(ticket_tile(tick[0]));   // published at least one barrier ago
+        if (t < ntiles) {
+          if ((iti + 1) & 1) tile_o = t;
+          else tile_e = t;
+          ++iti;
+          set_issue_tile(iti);
+          draw_ticket();
+        } else {
+          total = (iti + 1) * nst;       // every stage of this workgroup's stream is issued
+        }
+      } else {
+        if (++iti < myt) set_issue_tile(iti);
+      }
+    }
+  };
+  // DYN: wave 0 publishes a returned ticket (after the stage wait that covered its atomic)
+  bool tpend = false;
+  auto publish_ticket = [&]() {
+    if (w == 0 && tpend) {
+      const unsigned v = __builtin_amdgcn_readfirstlane(tkv);
+      if (lane == 0) tick[0] = v;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      tpend = false;
     }
   };
 
@@ -195,7 +251,25 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   uint4 hv[EPI == kEpiDGelu ? (C::MT + 1) / 2 : 1][EPI == kEpiDGelu ? 32 * SCH / 64 : 1];   // GELU' aux tile
   char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN>();
 
-  if (myt > 0) set_issue_tile(0);
+  if constexpr (DYN) {
+    // the first tile: drawn, published through LDS, then the second tile's ticket goes out
+    draw_ticket();
+    if (w == 0) {
+      const unsigned v = __builtin_amdgcn_readfirstlane(tkv);
+      if (lane == 0) tick[0] = v;
+    }
+    __syncthreads();
+    const int t0 = __builtin_amdgcn_readfirstlane(ticket_tile(tick[0]));
+    __syncthreads();            // every wave read the word before wave 0 publishes the next ticket
+    if (t0 >= ntiles) {
+      total = 0;                // this group's tiles are all taken: nothing to do
+    } else {
+      tile_e = t0;
+      draw_ticket();            // the ticket of this workgroup's second tile
+      tpend = true;
+    }
+  }
+  if (total > 0) set_issue_tile(0);
 #pragma unroll
   for (int q = 0; q < NS - 1; ++q)
     if (q < total) issue_next();
@@ -212,12 +286,19 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
       g8_wait_barrier<0>();
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (g + NS - 1 < total) issue_next();
+    if constexpr (DYN) {
+      publish_ticket();                    // covered by the vmcnt(0) above
+      const int it0 = iti;
+      if (g + NS - 1 < total) issue_next();
+      if (iti != it0) tpend = true;        // a new ticket atomic went out with this issue
+    } else {
+      if (g + NS - 1 < total) issue_next();
+    }
     if constexpr (EPI == kEpiDGelu) {
       // GELU' epilogue: the tile's aux (h) chunks are loaded in one batch at the start of its last
       // stage, so the epilogue's stores do not each wait out a dependent HBM round trip
       if (cst == nst - 1) {
-        const int t = b0 + cti * G;
+        const int t = DYN ? tile_of(cti) : b0 + cti * G;
         const int m0 = (t / tn) * BM + C::WM * wr, nw = (t % tn) * BN + C::WN * wc;
 #pragma unroll
         for (int ip = 0; ip < (C::MT + 1) / 2; ++ip)
@@ -254,7 +335,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
 
     // ---- epilogue of local tile cti.  acc[i][j] = D[n][m]: n = WN wc + 16 j + 4 fg + e,
     // m = 128 wr + 16 i + fr (tile-relative); through the wave's scratch 32 rows at a time
-    const int t = b0 + cti * G;
+    const int t = DYN ? tile_of(cti) : b0 + cti * G;
     ++cti;
     const int m0 = (t / tn) * BM + C::WM * wr, nw = (t % tn) * BN + C::WN * wc;
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -303,6 +384,18 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
     }
   }
   if (w >= 4) __builtin_amdgcn_s_setprio(0);
+  if constexpr (DYN) {
+    // this workgroup drew its ticket past its group's tiles (its stream ended on it): count it in
+    // the slot's done word; the last of the G workgroups resets the slot -- every draw of this
+    // launch has returned by then
+    if (threadIdx.x == 0) {
+      const unsigned d = __hip_atomic_fetch_add(a.ctr + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (unsigned)G - 1u) {
+        for (int x = 0; x < 8; ++x) __hip_atomic_store(a.ctr + 32 * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.ctr + 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 }  // namespace sae

@@ -44,6 +44,7 @@ struct NtArgs {
   long long lda, ldb, ldc, ldaux;
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
   int gp;              // kEpiGelu: c2 = gelu'(h) instead of h; kEpiDGelu: aux holds gelu'(h)
+  unsigned* ctr;       // gemm8 dynamic tile walk: {ticket, done} counters of this launch's slot
 };
 
 constexpr int kNtT = 128;   // output tile edge

@@ -87,6 +87,15 @@ def _sinking(bwd):
     return wrapped
 
 
+def occupy_cus(stream, workgroups: int, usec: float, threads: int = 256, lds_bytes: int = 64 * 1024) -> None:
+    """Diagnostic (``sae_occupy_cus``): ``workgroups`` workgroups that hold their CUs for ``usec``
+    microseconds on ``stream`` -- the CU footprint of an RCCL all-reduce's ring channels, for the
+    one-GPU contention emulation of the data-parallel step (bench.py --emulate-rccl)."""
+    lib = L.load()
+    L.check(lib.sae_occupy_cus(ctypes.c_void_p(stream.cuda_stream), int(workgroups), int(threads), int(lds_bytes),
+                               float(usec)))
+
+
 def set_kernel_timer(t):
     global _TIMER
     _TIMER = t

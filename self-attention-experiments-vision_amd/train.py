@@ -302,6 +302,17 @@ class TrainStep:
         # fatal in the watchdog).  The warm-up steps before the capture run without collectives.
         self._cpg = None
         self._comm_on = True
+        # one-GPU contention emulation of an N-GPU node (bench.py --emulate-rccl, env
+        # SAE_EMULATE_RCCL="channels,busbw_GBps,world[,lds_KiB[,threads]]"): beside each bucket's
+        # (one-rank) all-reduce, `channels` workgroups of `threads` threads holding `lds_KiB` of LDS
+        # (default 64 KiB, 256) occupy CUs on the communication stream for the ring time the bucket
+        # would take at `world` GPUs, 2 (world - 1) / world x bytes / busbw -- the CU footprint of
+        # RCCL's ring channels on the compute units the backward is using
+        self._emulate = None
+        em = os.environ.get("SAE_EMULATE_RCCL", "")
+        if em:
+            f = [float(x) for x in em.split(",")] + [64.0, 256.0][max(0, len(em.split(",")) - 3):]
+            self._emulate = (int(f[0]), f[1], int(f[2]), int(f[3] * 1024), int(f[4]))
         if self.collective in ("overlap", "between") and on_gpu:
             self._cpg = dist.new_group(backend="nccl", device_id=params[0].device)
         # world > 1: whether the step runs as a graph is decided by ALL ranks together (a host-side
@@ -430,6 +441,11 @@ class TrainStep:
             self._comm.wait_stream(torch.cuda.current_stream(t.device))
             with torch.cuda.stream(self._comm):
                 dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._cpg)
+                if self._emulate is not None:
+                    from . import ops
+                    ch, bw, wd, lds, thr = self._emulate
+                    usec = 2.0 * (wd - 1) / wd * t.numel() * 4 / (bw * 1e3)
+                    ops.occupy_cus(self._comm, ch, usec, threads=thr, lds_bytes=lds)
         else:
             self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-kernel register / spill / occupancy report for the HIP library (hipcc resource remarks).
-cd "$(dirname "$0")/.." && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -mllvm -amdgpu-mfma-vgpr-form=1 -fno-honor-nans -fno-slp-vectorize -I include \
+cd "$(dirname "$0")/.." && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -mllvm -amdgpu-mfma-vgpr-form=1 -fno-honor-nans -fno-slp-vectorize $REGS_FLAGS -I include \
   self-attention-experiments-vision_amd/csrc/capi.hip -o /tmp/_regs.so -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c "
 import sys,re,subprocess
 cur=None; rows={}
