@@ -254,6 +254,8 @@ def step_label(step, use_graph):
         base = "hip_graph_replay"
     coll = {"none": "no collective", "overlap": "rccl_allreduce overlapped with the backward",
             "between": "rccl_allreduce between the graphs", "host": "gloo host all-reduce between the graphs"}
+    if getattr(step, "_flagged", False) and use_graph and step.graph:
+        return f"{base} + rccl_allreduce per bucket on the comm stream, gated by device flags the backward sets"
     return f"{base} + {coll[step.collective]}"
 
 

@@ -402,6 +402,14 @@ int sae_smoothed_ce_bwd(void* stream, int32_t rows, int32_t classes, const void*
    ring time).  threads in [64, 1024], lds_bytes <= 160 KiB. */
 int sae_occupy_cus(void* stream, int32_t workgroups, int32_t threads, int32_t lds_bytes, float usec);
 
+/* Stream-ordered flags for collectives gated outside a HIP graph (train.py, the data-parallel step):
+   sae_flag_bump adds 1 to flags[index] (a one-thread kernel; system-scope atomic after the stream's
+   earlier kernels, whose writes the kernel boundary has made visible), so a graph can mark points of
+   its kernel chain without forking a branch; sae_stream_wait_flag makes `stream` wait until
+   *flag >= value (hipStreamWaitValue32, greater-or-equal) before its later work starts. */
+int sae_flag_bump(void* stream, uint32_t* flags, int32_t index);
+int sae_stream_wait_flag(void* stream, const uint32_t* flag, uint32_t value);
+
 /* Thread-local message describing the last failure on this thread ("" if none). */
 const char* sae_last_error(void);
 

@@ -94,6 +94,8 @@ _PROTOS = [
     ("sae_smoothed_ce_fwd", _i32, [_vp, _i32, _i32, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp]),
     ("sae_smoothed_ce_bwd", _i32, [_vp, _i32, _i32, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp, _i64]),
     ("sae_occupy_cus", _i32, [_vp, _i32, _i32, _i32, _f32]),
+    ("sae_flag_bump", _i32, [_vp, _vp, _i32]),
+    ("sae_stream_wait_flag", _i32, [_vp, _vp, ctypes.c_uint32]),
     ("sae_last_error", ctypes.c_char_p, []),
     ("sae_abi_version", _i32, []),
     ("sae_build_info", ctypes.c_char_p, []),

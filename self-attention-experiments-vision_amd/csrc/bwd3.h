@@ -122,7 +122,11 @@ template <int DP, int NW> struct B3Stage {
 // ROT: q / k rotated as they are staged (the K fragments also feed the K image, so dQ uses the
 // rotated K as it must), dq / dk rotated back as they are stored.
 // NSU: the 16-wide k-steps of S / dP that carry head-dim columns (3 for D = 48 at DP = 64)
-template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16>
+// STAG (8 waves, two per SIMD): waves 4-7 -- each the SIMD partner of one of waves 0-3 -- run the
+// previous tile's dQ product at the START of a step instead of at its end, so the two waves of a
+// SIMD are in different phases of the step (one's exponentials beside the other's MFMAs) instead of
+// in lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9); PRIO: waves 4-7 at s_setprio 1
+template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16, bool STAG = false, bool PRIO = false>
 __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void attn_bwd3_kernel(AttnArgs a) {
   using C = B3<DP, NW, KPW>;
   constexpr int NS = NSU, NT = C::NT, TB = C::TB, KS = C::KS;
@@ -303,6 +307,8 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
     const float* ldsD = ldsL + 32;
     char* img = dsb + bsel * C::DSIMG;
     if (qt + 1 < nqt) st.load(rq, rg, ro, a, qt + 1, rowoff, tid);
+    const bool late = STAG && w >= NW / 2;   // this wave runs the previous tile's dQ first
+    if (late && qt > 0) dq_tile(dsb + (bsel ^ 1) * C::DSIMG, qt - 1);
     if (active) {
       bf16x8 qr[NS], gr[NS];
 #pragma unroll
@@ -377,11 +383,12 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
         }
       }
     }
-    if (qt > 0) dq_tile(dsb + (bsel ^ 1) * C::DSIMG, qt - 1);
+    if (!late && qt > 0) dq_tile(dsb + (bsel ^ 1) * C::DSIMG, qt - 1);
     if (qt + 1 < nqt) st.template write<ROT>(smem + (bsel ^ 1) * TB, tid, &a.rope);
     __syncthreads();
     SAE_STAMP(3 + (qt < 26 ? qt : 26));
   };
+  if (PRIO && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
   {
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
@@ -390,6 +397,7 @@ __global__ __launch_bounds__(64 * NW, (NW * KPW == 8 && KPW == 1) ? 2 : 1) void 
       if (qt + 1 < nqt) step(qt + 1, B1{});
     }
   }
+  if (PRIO && w >= NW / 2) __builtin_amdgcn_s_setprio(0);
   dq_tile(dsb + ((nqt - 1) & 1) * C::DSIMG, nqt - 1);
   __syncthreads();   // every image read: the LDS becomes the per-wave store scratch
   SAE_STAMP(30);

@@ -313,14 +313,16 @@ template <int DP> int bwd2_run_agpr(hipStream_t st, const AttnArgs& a, bool pipe
 // (8 waves x 32 keys, two waves per SIMD); longer key ranges take the two-pass bwd2
 constexpr int kB3Keys = 256;
 
-template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16> int bwd3_run(hipStream_t st, const AttnArgs& a) {
+template <int DP, int NW, int KPW, bool ROT = false, int NSU = DP / 16, bool STAG = false, bool PRIO = false>
+int bwd3_run(hipStream_t st, const AttnArgs& a) {
   using C = B3<DP, NW, KPW>;
   static_assert(C::BK == kB3Keys, "bwd3 dispatch assumes 256-key blocks");
   const long long grid = (long long)a.H * a.B;
   if (a.Nk > C::BK) return fail(SAE_EINVAL, "bwd3: %d keys > %d", a.Nk, C::BK);
   if (grid > 0x7fffffffLL) return fail(SAE_EUNSUPPORTED, "grid too large");
-  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>, C::LDS)) return rc;
-  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT, NSU>), dim3((unsigned)grid), dim3(64 * NW), C::LDS, st, a);
+  if (int rc = lds_attr((const void*)attn_bwd3_kernel<DP, NW, KPW, ROT, NSU, STAG, PRIO>, C::LDS)) return rc;
+  hipLaunchKernelGGL((attn_bwd3_kernel<DP, NW, KPW, ROT, NSU, STAG, PRIO>), dim3((unsigned)grid), dim3(64 * NW),
+                     C::LDS, st, a);
   return check_launch("attn_bwd3");
 }
 
@@ -880,7 +882,8 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
                   "strides, no flags)");
     a.rope = *rope;
     hipStream_t st = (hipStream_t)stream;
-    if (a.Nk <= kB3Keys) return dp == 32 ? bwd3_run<32, 8, 1, true>(st, a) : bwd3_run<64, 8, 1, true>(st, a);
+    if (a.Nk <= kB3Keys)
+      return dp == 32 ? bwd3_run<32, 8, 1, true, 2, true>(st, a) : bwd3_run<64, 8, 1, true, 4, true>(st, a);
     return dp == 32 ? bwd2_run_default<32, true>(st, a) : bwd2_run_default<64, true>(st, a);
   }
   if (var != 1 && vec && cls_ok(d)) return cls_run<true>((hipStream_t)stream, a);
@@ -893,10 +896,18 @@ static int attn_bwd_impl(void* stream, const sae_attn_desc* d, const void* q, co
         if (dp == 32) return bwd3_run<32, 4, 2>(st, a);
         if (dp == 64) return bwd3_run<64, 4, 2>(st, a);
       }
+      if (var >= 5 && var <= 7 && dp == 64) {   // no stagger / stagger + priority / priority only
+        const bool d48 = d->head_dim <= 48;
+        if (var == 5) return d48 ? bwd3_run<64, 8, 1, false, 3>(st, a) : bwd3_run<64, 8, 1, false, 4>(st, a);
+        if (var == 6) return d48 ? bwd3_run<64, 8, 1, false, 3, true, true>(st, a) : bwd3_run<64, 8, 1, false, 4, true, true>(st, a);
+        return d48 ? bwd3_run<64, 8, 1, false, 3, false, true>(st, a) : bwd3_run<64, 8, 1, false, 4, false, true>(st, a);
+      }
 #endif
-      if (dp == 32) return bwd3_run<32, 8, 1>(st, a);
-      if (dp == 64 && d->head_dim <= 48) return bwd3_run<64, 8, 1, false, 3>(st, a);   // CaiT head_dim 48
-      if (dp == 64) return bwd3_run<64, 8, 1>(st, a);
+      // waves 4-7 staggered (the previous tile's dQ first): DeiT-S 53.6 -> 53.2 us, CaiT-S24
+      // 130.7 -> 128.3 us (profiles/r06g_bwd3_stagger_ab.txt; same sums, bit-identical results)
+      if (dp == 32) return bwd3_run<32, 8, 1, false, 2, true>(st, a);
+      if (dp == 64 && d->head_dim <= 48) return bwd3_run<64, 8, 1, false, 3, true>(st, a);   // CaiT head_dim 48
+      if (dp == 64) return bwd3_run<64, 8, 1, false, 4, true>(st, a);
     }
 #ifdef SAE_DEV_KNOBS
     if (dp == 64 && (var == 10 || var == 11)) return bwd2_run_agpr<64>(st, a, var == 11);
@@ -1324,6 +1335,24 @@ int sae_occupy_cus(void* stream, int32_t workgroups, int32_t threads, int32_t ld
   hipLaunchKernelGGL(occupy_cus_kernel, dim3((unsigned)workgroups), dim3((unsigned)threads), (size_t)lds_bytes,
                      (hipStream_t)stream, (long long)(usec * 100.f));
   return check_launch("occupy_cus");
+}
+
+__global__ void flag_bump_kernel(unsigned* flag) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int sae_flag_bump(void* stream, uint32_t* flags, int32_t index) {
+  if (!flags || index < 0) return fail(SAE_EINVAL, "flag_bump: flags must be non-NULL and index >= 0");
+  hipLaunchKernelGGL(flag_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned*)flags + index);
+  return check_launch("flag_bump");
+}
+
+int sae_stream_wait_flag(void* stream, const uint32_t* flag, uint32_t value) {
+  if (!flag || ((uintptr_t)flag & 3)) return fail(SAE_EINVAL, "stream_wait_flag: flag must be a non-NULL 4-byte-aligned pointer");
+  const hipError_t e = hipStreamWaitValue32((hipStream_t)stream, const_cast<uint32_t*>(flag), value,
+                                            hipStreamWaitValueGte, 0xffffffffu);
+  if (e != hipSuccess) return fail(SAE_EHIP, "hipStreamWaitValue32: %s", hipGetErrorString(e));
+  return ok();
 }
 
 int sae_gemm_nt_route(int32_t M, int32_t N, int32_t K, int32_t epilogue) {

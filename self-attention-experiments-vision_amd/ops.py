@@ -96,6 +96,22 @@ def occupy_cus(stream, workgroups: int, usec: float, threads: int = 256, lds_byt
                                float(usec)))
 
 
+def flag_bump(flags: torch.Tensor, index: int) -> None:
+    """flags[index] += 1 on the current stream (``sae_flag_bump``; flags int32 on the GPU): a mark in
+    a captured kernel chain that another stream can wait for (``stream_wait_flag``)."""
+    lib = L.load()
+    _require_gpu(flags)
+    L.check(lib.sae_flag_bump(_stream(flags), ctypes.c_void_p(flags.data_ptr()), int(index)))
+
+
+def stream_wait_flag(stream, flags: torch.Tensor, index: int, value: int) -> None:
+    """Make ``stream`` wait until flags[index] >= value (``sae_stream_wait_flag``)."""
+    lib = L.load()
+    _require_gpu(flags)
+    L.check(lib.sae_stream_wait_flag(ctypes.c_void_p(stream.cuda_stream),
+                                     ctypes.c_void_p(flags.data_ptr() + 4 * int(index)), int(value) & 0xffffffff))
+
+
 def set_kernel_timer(t):
     global _TIMER
     _TIMER = t

@@ -302,6 +302,17 @@ class TrainStep:
         # fatal in the watchdog).  The warm-up steps before the capture run without collectives.
         self._cpg = None
         self._comm_on = True
+        # "flagged" (graph steps with the overlapped collective, default on the GPU): the captured
+        # forward + backward stays ONE linear kernel chain -- at each bucket's ready point it bumps a
+        # device flag (sae_flag_bump) instead of forking the all-reduce onto the communication stream
+        # inside the graph -- and after each replay the host enqueues, on the communication stream,
+        # every bucket's wait for its flag (hipStreamWaitValue32) followed by its RCCL all-reduce,
+        # so the rings still run beside the rest of the backward.  A branch inside a replayed HIP graph
+        # costs the whole replay 0.13-0.4 ms on this runtime (the multi-queue launch path, measured
+        # with one-rank RCCL + a stand-in kernel per bucket: profiles/r06e_graph_fork.txt,
+        # r06d_rccl_emulation.txt); a linear graph keeps the single-queue fast path.  SAE_FLAGGED=0:
+        # the round-3 structure (the all-reduces forked inside the one graph).
+        self._flagged = False
         # one-GPU contention emulation of an N-GPU node (bench.py --emulate-rccl, env
         # SAE_EMULATE_RCCL="channels,busbw_GBps,world[,lds_KiB[,threads]]"): beside each bucket's
         # (one-rank) all-reduce, `channels` workgroups of `threads` threads holding `lds_KiB` of LDS
@@ -319,7 +330,10 @@ class TrainStep:
         # gloo group carries the one flag all-reduce): a rank whose capture fails must not run the
         # eager step while its peers replay graphs -- their collective sequences would differ
         self._flag_pg = dist.new_group(backend="gloo") if self.world > 1 and self.graph else None
-        self.two_graphs = self.collective in ("between", "host") or (self.collective == "none" and bool(two_graphs))
+        self._flagged = (self.collective == "overlap" and self.graph and on_gpu
+                         and os.environ.get("SAE_FLAGGED", "1") != "0")
+        self.two_graphs = (self.collective in ("between", "host") or (self.collective == "none" and bool(two_graphs))
+                           or self._flagged)
         if self.flat:
             # one flat fp32 gradient buffer, every .grad a 16-byte-aligned view into it (autograd
             # accumulates into the views in place), cut into buckets of ~bucket_cap_mb along
@@ -353,6 +367,11 @@ class TrainStep:
                 ops.set_grad_sinks(params, [p.grad for p in params])
             if self.collective == "overlap":
                 self._arm_overlap_hooks()
+            if self._flagged:
+                # one int32 counter per bucket, bumped once per replay of the forward + backward graph
+                self._flags = torch.zeros(len(self._buckets), dtype=torch.int32, device=dev)
+                self._flag_order = []   # bucket order of the captured bumps (the host's issue order)
+                self._epoch = 0
         # the sink-bound weight-gradient GEMMs run on a side stream beside the input-gradient chain
         # (ops.set_weight_grad_stream), opt-in: SAE_WG_STREAM=1 or wgrad_stream=True.  Off by default: the
         # concurrent dW kernels push the persistent gemm8 tiles into a tail (DeiT-S 15,381 vs
@@ -434,6 +453,12 @@ class TrainStep:
         self._launched[b] = True
         if not self._comm_on:   # the capture's warm-up steps: no collective
             return
+        if self._flagged and torch.cuda.is_current_stream_capturing():
+            # flagged graph: a mark on the captured chain; the collective is issued after the replay
+            from . import ops
+            ops.flag_bump(self._flags, b)
+            self._flag_order.append(b)
+            return
         if t.is_cuda:
             # the comm stream picks up everything enqueued so far on the compute stream (this
             # bucket's gradient kernels included) and runs the RCCL all-reduce beside the rest of
@@ -462,7 +487,8 @@ class TrainStep:
             if not self._launched[b]:
                 self._launch_bucket(b)
         if self._flat.is_cuda:
-            torch.cuda.current_stream(self._flat.device).wait_stream(self._comm)   # the join
+            if not (self._flagged and torch.cuda.is_current_stream_capturing()):
+                torch.cuda.current_stream(self._flat.device).wait_stream(self._comm)   # the join
         else:
             for w in self._works:
                 w.wait()
@@ -549,6 +575,25 @@ class TrainStep:
         for w in works:
             w.wait()
 
+    def _issue_flagged(self):
+        """After a replay of the flagged forward + backward graph: on the communication stream, each
+        bucket's wait for its flag (bumped by this replay) and its all-reduce, in the captured order;
+        the compute stream joins the communication stream before the optimizer's graph."""
+        from . import ops
+        self._epoch += 1
+        dev = self._flat.device
+        for b in self._flag_order:
+            lo, hi = self._buckets[b]
+            t = self._flat[lo:hi]
+            ops.stream_wait_flag(self._comm, self._flags, b, self._epoch)
+            with torch.cuda.stream(self._comm):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._cpg)
+                if self._emulate is not None:
+                    ch, bw, wd, lds, thr = self._emulate
+                    usec = 2.0 * (wd - 1) / wd * t.numel() * 4 / (bw * 1e3)
+                    ops.occupy_cus(self._comm, ch, usec, threads=thr, lds_bytes=lds)
+        torch.cuda.current_stream(dev).wait_stream(self._comm)
+
     def _eager(self, images: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         loss = self._fwd_bwd(images, labels)
         self._allreduce()
@@ -613,6 +658,8 @@ class TrainStep:
                 self._g = g
             else:                 # the collectives stay outside: two graphs around them
                 g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                if self._flagged:
+                    self._flag_order = []
                 with torch.cuda.graph(g, capture_error_mode=mode):
                     self._loss = self._fwd_bwd(self._images, self._labels)
                 with torch.cuda.graph(go, capture_error_mode=mode):
@@ -679,6 +726,9 @@ class TrainStep:
             self.opt.refresh_if_stale()
         self._g.replay()
         if self._g_opt is not None:
-            self._allreduce()
+            if self._flagged:
+                self._issue_flagged()
+            else:
+                self._allreduce()
             self._g_opt.replay()
         return self._loss

@@ -147,8 +147,9 @@ def test_grad_sink_follows_param_grad(dev):
     ops.set_grad_sinks(None)
 
 
+@pytest.mark.parametrize("flagged", ["1", "0"])
 @pytest.mark.parametrize("model", ["deit_ti_patch16", "cait"])
-def test_world1_rccl_overlapped_step(dev, model):
+def test_world1_rccl_overlapped_step(dev, model, flagged):
     """The multi-rank step's collective path on one GPU (tests/world1_rccl_case.py): a one-rank
     RCCL group, the bucket all-reduces launched from inside the backward on the communication
     stream and captured with the rest of the step in ONE HIP graph; losses and parameters equal to
@@ -159,9 +160,10 @@ def test_world1_rccl_overlapped_step(dev, model):
     import sys
     import os
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "world1_rccl_case.py")
-    r = subprocess.run([sys.executable, "-u", script, model], capture_output=True, text=True, timeout=110)
+    env = dict(os.environ, SAE_FLAGGED=flagged)   # the default flag-gated structure / the in-graph fork
+    r = subprocess.run([sys.executable, "-u", script, model], capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0 and "WORLD1_OK" in r.stdout, \
-        f"rc {r.returncode}\nstdout:\n{r.stdout[-2000:]}\nstderr:\n{r.stderr[-4000:]}"
+        f"SAE_FLAGGED={flagged} rc {r.returncode}\nstdout:\n{r.stdout[-2000:]}\nstderr:\n{r.stderr[-4000:]}"
 
 
 def test_fused_adamw_cast_copies(dev):

@@ -3,8 +3,9 @@
     python tests/world1_rccl_case.py <deit_ti_patch16 | cait>
 
 The multi-rank step's collective path on one GPU: a one-rank RCCL group (backend nccl), the
-bucket all-reduces launched from inside the backward on the communication stream and captured
-with the rest of the step in ONE HIP graph (train.py "overlap").  A one-rank SUM is the identity,
+bucket all-reduces on the communication stream, overlapped with the backward: gated by device flags
+the captured (linear) backward graph bumps (train.py "flagged", the default), or with SAE_FLAGGED=0
+forked inside ONE HIP graph with the rest of the step (train.py "overlap").  A one-rank SUM is the identity,
 so losses and parameters must equal the no-collective graph step's bit for bit; the buckets must
 all have been launched, the first before the backward finished.  Prints WORLD1_OK on success.
 """
@@ -47,10 +48,18 @@ def main(model):
                  torch.randint(0, 1000, (8,), device=dev, generator=g)) for _ in range(3)]
         la = [float(s_a(x, y)) for x, y in data]
         lb = [float(s_b(x, y)) for x, y in data]
-        assert s_b._g is not None and s_b._g_opt is None and s_b.graph   # one graph, collectives inside
         nb = len(s_b._buckets)
         assert sorted(bi for bi, _ in order[-nb:]) == list(range(nb))     # the captured backward's launches
         assert order[-nb][1] < len(s_b._params)                            # the first before the last gradient
+        if os.environ.get("SAE_FLAGGED", "1") != "0":
+            # flagged: a linear forward + backward graph with one flag bump per bucket, the optimizer's
+            # graph, and the all-reduces issued per replay behind the flags (one per bucket per replay)
+            assert s_b._flagged and s_b._g is not None and s_b._g_opt is not None and s_b.graph
+            assert sorted(s_b._flag_order) == list(range(nb))
+            torch.cuda.synchronize()
+            assert s_b._flags.tolist() == [len(data)] * nb, s_b._flags.tolist()
+        else:
+            assert s_b._g is not None and s_b._g_opt is None and s_b.graph   # one graph, collectives inside
         assert la == lb, (la, lb)
         for (n, pa), pb in zip(m_a.named_parameters(), m_b.parameters()):
             assert torch.equal(pa, pb), n
