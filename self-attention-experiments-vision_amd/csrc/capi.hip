@@ -542,15 +542,15 @@ static int dw_launch(const DwArgs& a, bool bias, long long grid, size_t lds, hip
 }
 
 // the LDS-DMA form of the plain weight-gradient kernel (gemm_dw8.h)
-template <int NG, int NS = kDw8NS>
+template <int NG, int NS = kDw8NS, int STAG = 0>
 static int dw8_launch(const DwArgs& a, bool bias, long long grid, hipStream_t st) {
   constexpr int lds = dw8_lds_bytes<NG, NS>();
-  const void* fn = bias ? (const void*)gemm_dw8_kernel<true, NG, NS> : (const void*)gemm_dw8_kernel<false, NG, NS>;
+  const void* fn = bias ? (const void*)gemm_dw8_kernel<true, NG, NS, STAG> : (const void*)gemm_dw8_kernel<false, NG, NS, STAG>;
   if (int rc = lds_attr(fn, lds)) return rc;
   if (bias)
-    hipLaunchKernelGGL((gemm_dw8_kernel<true, NG, NS>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+    hipLaunchKernelGGL((gemm_dw8_kernel<true, NG, NS, STAG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
   else
-    hipLaunchKernelGGL((gemm_dw8_kernel<false, NG, NS>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
+    hipLaunchKernelGGL((gemm_dw8_kernel<false, NG, NS, STAG>), dim3((unsigned)grid), dim3(256 * NG), lds, st, a);
   return 0;
 }
 
@@ -1224,8 +1224,16 @@ static int gemm_dw_impl(void* stream, int32_t M, int32_t I, int32_t J, const voi
 #endif
   if (dma && dw8v == 1) {
     if (int rc = dw8_launch<1, 8>(a, db != nullptr, grid, st)) return rc;
+#ifdef SAE_DEV_KNOBS
+  } else if (dma && NG == 2 && (dw8v == 2 || dw8v == 3)) {   // wave-group offset A/B: none / a whole stage
+    if (int rc = dw8v == 2 ? dw8_launch<2, kDw8NS, 0>(a, db != nullptr, grid, st)
+                           : dw8_launch<2, kDw8NS, 1>(a, db != nullptr, grid, st))
+      return rc;
+#endif
   } else if (dma) {
-    if (int rc = NG == 2 ? dw8_launch<2>(a, db != nullptr, grid, st) : dw8_launch<1>(a, db != nullptr, grid, st))
+    // two wave groups half a stage apart (STAG 2): DeiT-S step 8.148 -> 8.056 ms same box
+    // (profiles/r06h_dw8_stagger_ab.txt); a whole stage apart measured level
+    if (int rc = NG == 2 ? dw8_launch<2, kDw8NS, 2>(a, db != nullptr, grid, st) : dw8_launch<1>(a, db != nullptr, grid, st))
       return rc;
   } else if (NG == 2) {
     if (int rc = dw_launch<XR, YR, 2>(a, db != nullptr, grid, lds, st)) return rc;

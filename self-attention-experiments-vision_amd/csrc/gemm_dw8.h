@@ -44,8 +44,13 @@ template <int N> __device__ __forceinline__ void dw8_wait(int ahead) {
   }
 }
 
-template <bool BIAS, int NG, int NS = kDw8NS>
+// STAG (NG = 2; dev A/B): the two wave groups (waves 0-3 / 4-7, SIMD partners) offset by one
+// barrier -- 1: one barrier per stage (a whole stage apart); 2: a second barrier between the two
+// k-steps of a stage (half a stage apart) -- so that partners do not read LDS and issue MFMAs in
+// lockstep.  Each group reads only its own ring, so the offset moves no data hazard.
+template <bool BIAS, int NG, int NS = kDw8NS, int STAG = 0>
 __global__ __launch_bounds__(256 * NG, NG == 1 && NS <= 4 ? 2 : 1) void gemm_dw8_kernel(DwArgs a) {
+  static_assert(STAG == 0 || NG == 2, "stagger: two wave groups");
   extern __shared__ __attribute__((aligned(16))) char smem_all[];
   const int ti = (a.I + kDwT - 1) / kDwT, tj = (a.J + kDwT - 1) / kDwT;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);   // as gemm_dw_kernel: a chunk's tiles on one XCD
@@ -118,6 +123,7 @@ __global__ __launch_bounds__(256 * NG, NG == 1 && NS <= 4 ? 2 : 1) void gemm_dw8
 #pragma unroll
   for (int q = 0; q < NS - 1; ++q)
     if (q < nst) issue(q);
+  if (STAG && grp == 1) asm volatile("s_barrier" ::: "memory");   // the offset
   for (int g = 0; g < nst; ++g) {
     dw8_wait<NS - 2>(min(NS - 2, nst - 1 - g));   // younger stages still in flight
     __builtin_amdgcn_sched_barrier(0);
@@ -126,6 +132,10 @@ __global__ __launch_bounds__(256 * NG, NG == 1 && NS <= 4 ? 2 : 1) void gemm_dw8
     const char* imy = imx + kDw8Img;
 #pragma unroll
     for (int k = 0; k < kDw8K / 16; ++k) {
+      if (STAG == 2 && k == 1) {
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
       const bf16x8 a0 = dw_colfrag(imx, ca, k, 0), a1 = dw_colfrag(imx, ca, k, 1);
       const bf16x8 b0 = dw_colfrag(imy, ca + 4, k, 0), b1 = dw_colfrag(imy, ca + 4, k, 1);
       acc[0][0] = MF<__bf16>::mma(a0, b0, acc[0][0]);
@@ -138,6 +148,7 @@ __global__ __launch_bounds__(256 * NG, NG == 1 && NS <= 4 ? 2 : 1) void gemm_dw8
       }
     }
   }
+  if (STAG && grp == 0) asm volatile("s_barrier" ::: "memory");   // balance the offset
   if constexpr (NG == 2) {
     // group 1 hands its accumulators to group 0 through the (now idle) ring, as gemm_dw_kernel
     __syncthreads();
