@@ -643,6 +643,13 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
 }
 template <int EPI, int BN, int BK, int NS>
 static int g8_launch(const NtArgs& g, hipStream_t st) {
+#ifdef SAE_DEV_KNOBS
+  if constexpr (BK == 64 && NS == 2) {   // dev A/B: 32-deep stages, 4-deep ring (three stages in flight)
+    if (dev_knob("SAE_G8_DEPTH") == 1)
+      return g8_pick_bm(g.M, g.N, BN) == 224 ? g8_launch_bm<EPI, BN, 32, 4, 224>(g, st)
+                                             : g8_launch_bm<EPI, BN, 32, 4, 256>(g, st);
+  }
+#endif
   return g8_pick_bm(g.M, g.N, BN) == 224 ? g8_launch_bm<EPI, BN, BK, NS, 224>(g, st)
                                          : g8_launch_bm<EPI, BN, BK, NS, 256>(g, st);
 }
