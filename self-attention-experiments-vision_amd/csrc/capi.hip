@@ -411,22 +411,27 @@ template <typename T, int DP, bool VEC> int th_bwd_run(hipStream_t st, ThArgs a)
 
 // bf16 with the head mixes on the MFMA (th2.h).  H <= 8: one wave per head (NWMAX 8).  9..16 heads:
 // two heads per wave (eight waves of <= 256 registers; sixteen waves of 128 spilled heavily).
-template <int DP, int NWMAX, bool ROT, int HPW, bool LEAN = false> int th2_fwd_run(hipStream_t st, const ThArgs& a) {
+template <int DP, int NWMAX, bool ROT, int HPW, bool LEAN = false, int NSU = DP / 16>
+int th2_fwd_run(hipStream_t st, const ThArgs& a) {
   const int nqb = (a.Nq + 31) / 32, nw = (a.H + HPW - 1) / HPW;
   const size_t lds = th2_lds_bytes<DP, NWMAX * HPW <= 8>(a.H, 1, LEAN);
-  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>, lds)) return rc;
-  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
+  if (int rc = lds_attr((const void*)th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN, NSU>, lds)) return rc;
+  hipLaunchKernelGGL((th2_fwd_kernel<DP, NWMAX, ROT, HPW, LEAN, NSU>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   return check_launch("th2_fwd");
 }
 
-template <int DP, int NWMAX, bool ROT, int HPW> int th2_bwd_run(hipStream_t st, ThArgs a) {
+// LEAN: the query pass at two workgroups per CU (the key pass LEAN -- K / V / Q / dO re-read per
+// query tile, 13 spilled registers -- measured 306 vs 230 us: profiles/r06t_th_kv_lean_rejected.txt)
+template <int DP, int NWMAX, bool ROT, int HPW, bool LEAN = false, int NSU = DP / 16>
+int th2_bwd_run(hipStream_t st, ThArgs a) {
   constexpr bool KST = NWMAX * HPW <= 8;
   const int nqb = (a.Nq + 31) / 32, nkb = (a.Nk + 31) / 32, nw = (a.H + HPW - 1) / HPW;
   a.nblk = nqb * a.B;
-  const size_t lds = th2_lds_bytes<DP, KST>(a.H, HPW), lds_kv = th2_kv_lds_bytes<DP, KST>(a.H, KST && HPW == 1);
-  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>, lds)) return rc;
+  const size_t lds = th2_lds_bytes<DP, KST>(a.H, LEAN ? 2 : HPW);
+  const size_t lds_kv = th2_kv_lds_bytes<DP, KST>(a.H, KST && HPW == 1);
+  if (int rc = lds_attr((const void*)th2_bwd_q_kernel<DP, NWMAX, ROT, HPW, LEAN, NSU>, lds)) return rc;
   if (int rc = lds_attr((const void*)th2_bwd_kv_kernel<DP, NWMAX, ROT, HPW>, lds_kv)) return rc;
-  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT, HPW>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
+  hipLaunchKernelGGL((th2_bwd_q_kernel<DP, NWMAX, ROT, HPW, LEAN, NSU>), dim3(nqb * a.B), dim3(64 * nw), lds, st, a);
   if (int rc = check_launch("th2_bwd_q")) return rc;
   hipLaunchKernelGGL((th2_bwd_kv_kernel<DP, NWMAX, ROT, HPW>), dim3(nkb * a.B), dim3(64 * nw), lds_kv, st, a);
   if (int rc = check_launch("th2_bwd_kv")) return rc;
@@ -436,11 +441,21 @@ template <int DP, int NWMAX, bool ROT, int HPW> int th2_bwd_run(hipStream_t st, 
 
 // <= 8 heads: the forward at <= 128 VGPRs, two workgroups per CU (CaiT-S24 207 -> 184 us,
 // profiles/r05v_th_lean_ab.txt)
+// round 6, DP 64 at D <= 48 (every CaiT width): three head-dim k-steps (NSU 3) -- the forward fits
+// 128 VGPRs without spills (its scratch traffic was 1.4x the algorithmic bytes: 172 -> 160 us at
+// CaiT-S24, 1.05x; profiles/r06s_th_lean_ab.txt)
 template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
+  if constexpr (DP == 64)
+    if (a.H <= 8 && !a.rope.sin && a.D <= 48) return th2_fwd_run<64, 8, false, 1, true, 3>(st, a);
   if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true, 1, true>(st, a) : th2_fwd_run<DP, 8, true, 2>(st, a);
   return a.H <= 8 ? th2_fwd_run<DP, 8, false, 1, true>(st, a) : th2_fwd_run<DP, 8, false, 2>(st, a);
 }
+// round 6: the query pass LEAN (two workgroups per CU) at <= 8 heads without rotary (CaiT-S24
+// backward 540 -> 474 us; profiles/r06s_th_lean_ab.txt)
 template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
+  if constexpr (DP == 64)
+    if (a.H <= 8 && !a.rope.sin && !dev_knob("SAE_TH_BWDQ_WIDE"))
+      return a.D <= 48 ? th2_bwd_run<64, 8, false, 1, true, 3>(st, a) : th2_bwd_run<64, 8, false, 1, true>(st, a);
   if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true, 1>(st, a) : th2_bwd_run<DP, 8, true, 2>(st, a);
   return a.H <= 8 ? th2_bwd_run<DP, 8, false, 1>(st, a) : th2_bwd_run<DP, 8, false, 2>(st, a);
 }

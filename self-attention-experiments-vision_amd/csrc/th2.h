@@ -242,10 +242,12 @@ __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* o
 // sixteen of 128, which spilled); wave w owns heads w + NW e, e < HPW, NW = ceil(H / HPW) waves.
 // LEAN: <= 128 VGPRs (four waves per SIMD: two workgroups per CU at <= 8 heads) -- no K prefetch,
 // mix groups of two
-template <int DP, int NWMAX, bool ROT = false, int HPW = 1, bool LEAN = false>
+// NSU: 16-wide head-dim k-steps held and multiplied (D <= 16 NSU; CaiT's D = 48 at DP 64: 3, which
+// frees the registers of an all-zero fourth Q / K fragment)
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1, bool LEAN = false, int NSU = DP / 16>
 __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
-  constexpr int NS = DP / 16, NT = DP / 32;
+  constexpr int NS = NSU, NT = DP / 32;
   constexpr bool KST = NWMAX * HPW <= 8;     // H <= 8: stacked mixes, heads in registers 0..3
   constexpr int NR = KST ? 4 : 8;            // registers r < NR hold the mixed heads row_of(r, h)
   constexpr int IMG = th2_img<KST>();
@@ -279,7 +281,8 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
   th2_zero_pad<KST>(XS, H, tid, 64 * NW);
   th2_zero_pad<KST>(XP, H, tid, 64 * NW);
   constexpr bool rot = ROT;   // rotary: q / k rotated as they are loaded
-  const bool full = a.D > 16 * (NS - 1);   // the last 16-wide k-step holds head-dim columns
+  // the last 16-wide k-step holds head-dim columns (NSU < DP / 16: dispatched for 16 (NSU - 1) < D)
+  const bool full = NSU < DP / 16 || a.D > 16 * (NS - 1);
   bf16x8 qf[HPW][NS];
 #pragma unroll
   for (int e = 0; e < HPW; ++e)
@@ -326,14 +329,14 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) kn[s_] = th2_frag(rK[e], kt * 32 + r32, a.ks[1], a.D, s_, h);
   };
-  auto scores = [&](int kt) {
+  auto scores = [&](int kt, int ktn) {   // ktn: the tile whose K fragments PF prefetches
 #pragma unroll
     for (int e = 0; e < HPW; ++e) {
       if constexpr (!PF) load_k(e, kt);
       bf16x8 kc[NS];
 #pragma unroll
       for (int s_ = 0; s_ < NS; ++s_) kc[s_] = rot ? rope8<1>(kn[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h) : kn[s_];
-      if constexpr (PF) load_k(0, kt + 1 < nkt ? kt + 1 : 0);
+      if constexpr (PF) load_k(0, ktn);
       f32x16 s = zero16();
 #pragma unroll
       for (int s_ = 0; s_ < NS; ++s_)
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
   };
   if constexpr (PF) load_k(0, 0);
   for (int kt = 0; kt < nkt; ++kt) {
-    scores(kt);
+    scores(kt, kt + 1 < nkt ? kt + 1 : nkt - 1);   // (the last prefetch: pass 1's first tile)
     __syncthreads();
     stats(kt);
     __syncthreads();
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
   auto probs = [&](int kt) {   // this wave's blocks of tile kt: P2 = T2^T P into XP
     const char* xs = XS;
     char* xp = XP;
-    constexpr int G = KST && !LEAN ? 4 : 2;   // blocks per group: independent chains issued together
+    constexpr int G = KST && !LEAN ? 4 : (LEAN && NSU < DP / 16 ? 1 : 2);   // blocks per group: independent chains issued together
     const bool whole = kt * 32 + 32 <= a.Nk;   // every key of the tile exists (wave-uniform)
     for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 c[G];
@@ -448,37 +451,59 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
           acco[e][t] = MF<__bf16>::mma(I::colfrag(ldsV[e], 0, s2, 32 * t, lane), pf, acco[e][t]);
       }
   };
-  WStage<__bf16, DP, true> vst[HPW];   // V tile kt + 1 in flight while tile kt computes (wave-private images)
+  // pass 1 sweeps the key tiles in reverse: the tiles pass 0 read last are the most recently used
+  // in L2 (the forward's excess reads, 1.37x, turned out to be its spilled registers' scratch
+  // traffic, gone with NSU 3: profiles/r06p_th_traffic.txt)
+  WStage<__bf16, DP, true> vst[HPW];   // V tile kt - 1 in flight while tile kt computes (wave-private images)
 #pragma unroll
   for (int e = 0; e < HPW; ++e) {
-    vst[e].load_buf(rV[e], 0, a.vs[1], a.D, lane);
+    vst[e].load_buf(rV[e], (nkt - 1) * 32, a.vs[1], a.D, lane);
     vst[e].write(ldsV[e], lane);
   }
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt)
+  for (int kt = nkt - 1; kt >= 0; --kt) {
+    if (kt > 0)
 #pragma unroll
-      for (int e = 0; e < HPW; ++e) vst[e].load_buf(rV[e], (kt + 1) * 32, a.vs[1], a.D, lane);
-    scores(kt);
+      for (int e = 0; e < HPW; ++e) vst[e].load_buf(rV[e], (kt - 1) * 32, a.vs[1], a.D, lane);
+    scores(kt, kt > 0 ? kt - 1 : 0);
     __syncthreads();
     probs(kt);
     __syncthreads();
     pv();
-    if (kt + 1 < nkt)   // wave-private: after this wave's own reads
+    if (kt > 0)   // wave-private: after this wave's own reads
 #pragma unroll
       for (int e = 0; e < HPW; ++e) vst[e].write(ldsV[e], lane);
     __syncthreads();
   }
-  if (q < a.Nq) {
+  // O through LDS: the workgroup holds every head of its 32 queries, i.e. whole token rows of the
+  // [B, N, H, D] output; staged as [query][head][d] and stored in 16-byte chunks, consecutive lanes on
+  // consecutive chunks (instead of 8-byte pieces of 96-byte head rows per lane)
+  {
+    const int rowb = H * a.D * 2 + 16;   // bytes per staged query row (+16: spreads the rows' banks)
 #pragma unroll
     for (int e = 0; e < HPW; ++e) {
       if (!hv[e]) continue;
-      __bf16* O = reinterpret_cast<__bf16*>(a.o) + b * a.os[0] + hd[e] * a.os[2] + (long long)q * a.os[1];
+      char* rp = smem + r32 * rowb + hd[e] * a.D * 2;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          store4<__bf16, true>(O, 32 * t + 8 * g + 4 * h, a.D, acco[e][t][4 * g], acco[e][t][4 * g + 1],
-                               acco[e][t][4 * g + 2], acco[e][t][4 * g + 3]);
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = 32 * t + 8 * g + 4 * h;
+          if (d0 < a.D) {
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            const bf16x4 v = {(__bf16)acco[e][t][4 * g], (__bf16)acco[e][t][4 * g + 1], (__bf16)acco[e][t][4 * g + 2],
+                              (__bf16)acco[e][t][4 * g + 3]};
+            *reinterpret_cast<bf16x4*>(rp + d0 * 2) = v;
+          }
+        }
+    }
+    __syncthreads();
+    const int cpd = a.D / 8, cpr = H * cpd;   // 16-byte chunks per head row / per query row
+    const int nq = min(32, a.Nq - qb * 32);
+    __bf16* const O = reinterpret_cast<__bf16*>(a.o) + b * a.os[0] + (long long)(qb * 32) * a.os[1];
+    for (int c = tid; c < nq * cpr; c += 64 * NW) {
+      const int r = c / cpr, rem = c - r * cpr, hh = rem / cpd, dc = rem - hh * cpd;
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + r * rowb + (hh * a.D + 8 * dc) * 2);
+      *reinterpret_cast<uint4*>(O + (long long)r * a.os[1] + hh * a.os[2] + 8 * dc) = v;
     }
   }
 }
@@ -486,10 +511,13 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_fwd_kernel(ThArg
 // ============================================================================ bwd: query
 // pass A: delta_i = rowsum(P_i o dP_i), dP = T2 dP2, dP2_j = dO_j V_j^T; dT2 = sum P (x) dP2.
 // pass B: dS1 = P o (dP - delta), dT1 = sum S (x) dS1, dS = T1 dS1, dQ_w += scale dS_w K_w.
-template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
-__global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
+// LEAN (H <= 8): <= 128 VGPRs, two workgroups per CU -- mix operands in the LDS table, no K / V
+// prefetch, one mix chain per group (the forward's LEAN recipe)
+template <int DP, int NWMAX, bool ROT = false, int HPW = 1, bool LEAN = false, int NSU = DP / 16>
+__global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThArgs a) {
+  static_assert(!LEAN || HPW == 1, "LEAN: one head per wave");
   using I = Img<__bf16, DP>;
-  constexpr int NS = DP / 16, NT = DP / 32;
+  constexpr int NS = NSU, NT = DP / 32;   // (NSU as in th2_fwd_kernel)
   constexpr bool KST = NWMAX * HPW <= 8;
   constexpr int NR = KST ? 4 : 8;
   constexpr int IMG = th2_img<KST>();
@@ -524,6 +552,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   th2_zero_pad<KST>(XS, H, tid, 64 * NW);
   th2_zero_pad<KST>(XG, H, tid, 64 * NW);
   constexpr bool rot = ROT;   // rotary: q / k rotated as loaded, dq rotated back
+  // (a compile-time `full` for NSU < DP / 16, as in th2_fwd_kernel, spilled 12 registers here vs 4;
+  // re-reading the dO fragments per tile instead of holding them: no spills but 508 vs 474 us)
   const bool full = a.D > 16 * (NS - 1);
   bf16x8 qf[HPW][NS], gf[HPW][NS];
 #pragma unroll
@@ -538,7 +568,8 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   // wave 0 writes before the first barrier (the registers go to the second head's operands)
   Th2Mix m1r, m2tr, m1tr;
   char* const mxt = smem + 2 * IMG + H * I::bytes(32);
-  if constexpr (HPW == 1) {
+  constexpr bool MXR = HPW == 1 && !LEAN;   // mix operands held in registers
+  if constexpr (MXR) {
     m1r = th2_mix<false, false, KST>(a.th1, H, lane, kLog2e);   // S1 = T1^T S, log2 domain (image)
     m2tr = th2_mix<true, false, KST>(a.th2, H, lane);    // dP = T2 dP2        (image)
     m1tr = th2_mix<true, true, KST>(a.th1, H, lane);     // dS = T1 dS1        (accumulator)
@@ -547,9 +578,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
     th2_mx_put(mxt, 3, 1, lane, th2_mix<true, false, KST>(a.th2, H, lane));
     th2_mx_put(mxt, 3, 2, lane, th2_mix<true, true, KST>(a.th1, H, lane));
   }
-  auto m1 = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1r; else return th2_mx_get(mxt, 3, 0, lane); };
-  auto m2t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m2tr; else return th2_mx_get(mxt, 3, 1, lane); };
-  auto m1t = [&]() -> Th2Mix { if constexpr (HPW == 1) return m1tr; else return th2_mx_get(mxt, 3, 2, lane); };
+  auto m1 = [&]() -> Th2Mix { if constexpr (MXR) return m1r; else return th2_mx_get(mxt, 3, 0, lane); };
+  auto m2t = [&]() -> Th2Mix { if constexpr (MXR) return m2tr; else return th2_mx_get(mxt, 3, 1, lane); };
+  auto m1t = [&]() -> Th2Mix { if constexpr (MXR) return m1tr; else return th2_mx_get(mxt, 3, 2, lane); };
   // lse (log2 domain) of the mixed rows of this lane's query, register r <-> head row_of(r, h)
   float lse2[NR];
 #pragma unroll
@@ -560,7 +591,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   const int nkt = (a.Nk + 31) / 32;
   // next key tile's K / V fragments, in flight while this one computes (one head per wave: with
   // two, the registers go to the second head's operands instead and the loads are direct)
-  constexpr bool PF = HPW == 1;
+  constexpr bool PF = HPW == 1 && !LEAN;
   bf16x8 kn[NS], vn[NS];
   auto load_kv = [&](int e, int kt) {
 #pragma unroll
@@ -572,6 +603,37 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   // S_h -> XS, dP2_h -> XG for this wave's heads; stage_k: the (rotated) K fragments also form the
   // head's K image, the dQ product's operand (key rows, the WStage layout)
   auto tiles = [&](int kt, bool stage_k) {
+    if constexpr (LEAN) {   // one operand set and one accumulator live at a time: K -> S, then V -> dP2
+      f32x16 s = zero16();
+      {
+        bf16x8 kc[NS];
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_) {
+          kc[s_] = th2_frag(rK[0], kt * 32 + r32, a.ks[1], a.D, s_, h);
+          if (rot) kc[s_] = rope8<1>(kc[s_], a.rope, kt * 32 + r32, 16 * s_ + 8 * h);
+        }
+        if (stage_k)
+#pragma unroll
+          for (int s_ = 0; s_ < DP / 16; ++s_)   // (columns past NSU k-steps: zero)
+            *reinterpret_cast<bf16x8*>(ldsK[0] + r32 * (DP * 2) + 16 * ((2 * s_ + h) ^ swz<DP>(r32))) =
+                s_ < NS ? kc[s_ < NS ? s_ : 0] : bf16x8{};
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_)
+          if (s_ < NS - 1 || full) s = MF<__bf16>::mma(qf[0][s_], kc[s_], s);
+      }
+      if (hv[0]) th2_put(XS, hd[0], s, a.scale, lane);
+      f32x16 g = zero16();
+      {
+        bf16x8 vc[NS];
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_) vc[s_] = th2_frag(rV[0], kt * 32 + r32, a.vs[1], a.D, s_, h);
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_)
+          if (s_ < NS - 1 || full) g = MF<__bf16>::mma(gf[0][s_], vc[s_], g);
+      }
+      if (hv[0]) th2_put(XG, hd[0], g, 1.f, lane);
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < HPW; ++e) {
       if constexpr (!PF) load_kv(e, kt);
@@ -584,8 +646,9 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
       if constexpr (PF) load_kv(0, kt + 1 < nkt ? kt + 1 : 0);
       if (stage_k)
 #pragma unroll
-        for (int s_ = 0; s_ < NS; ++s_)
-          *reinterpret_cast<bf16x8*>(ldsK[e] + r32 * (DP * 2) + 16 * ((2 * s_ + h) ^ swz<DP>(r32))) = kc[s_];
+        for (int s_ = 0; s_ < DP / 16; ++s_)   // (columns past NSU k-steps: zero)
+          *reinterpret_cast<bf16x8*>(ldsK[e] + r32 * (DP * 2) + 16 * ((2 * s_ + h) ^ swz<DP>(r32))) =
+              s_ < NS ? kc[s_ < NS ? s_ : 0] : bf16x8{};
       f32x16 s = zero16(), g = zero16();
 #pragma unroll
       for (int s_ = 0; s_ < NS; ++s_) {
@@ -610,7 +673,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   for (int kt = 0; kt < nkt; ++kt) {
     tiles(kt, false);
     __syncthreads();
-    constexpr int G = 2;   // blocks per group: independent chains issued together
+    constexpr int G = LEAN ? 1 : 2;   // blocks per group: independent chains issued together
     for (int b0 = w; b0 < 32 && kt * 32 + b0 < a.Nk; b0 += G * NW) {
       f32x16 p[G], dp[G];
 #pragma unroll
@@ -666,7 +729,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_q_kernel(ThArgs a) {
   for (int kt = 0; kt < nkt; ++kt) {
     tiles(kt, true);   // (wave-private K images: after this wave's previous dQ reads)
     __syncthreads();
-    constexpr int G = HPW == 1 ? 2 : 1;   // (two heads per wave: one chain, the registers are short)
+    constexpr int G = HPW == 1 && !LEAN ? 2 : 1;   // (two heads per wave / LEAN: one chain, the registers are short)
     for (int b0 = w; b0 < 32; b0 += G * NW) {
       f32x16 ds1[G], dp[G];
 #pragma unroll

@@ -44,6 +44,7 @@ def main():
                     help="BoTNet relative logits (square Hs = Ws = sqrt(Nk) grid, N(0, 1/D) bias tables)")
     ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B (dev build: SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so)")
     ap.add_argument("--bwd-variants", default="", help="comma list of SAE_BWD_VARIANT values to A/B")
+    ap.add_argument("--knob", default="", help="NAME=v1,v2,...: any dev-library knob to A/B (dev build)")
     args = ap.parse_args()
     import torch
     import sae_vision_amd.ops as ops
@@ -54,10 +55,15 @@ def main():
     results = {}
     fv = args.fwd_variants.split(",") if args.fwd_variants else [os.environ.get("SAE_FWD_VARIANT", "")]
     bv = args.bwd_variants.split(",") if args.bwd_variants else [os.environ.get("SAE_BWD_VARIANT", "")]
-    runs = [(n, f, b) for n in args.shapes.split(",") for f in fv for b in bv]
-    for shape, fvar, bvar in runs:
+    kname, kvals = (args.knob.split("=") + [""])[:2] if args.knob else ("", "")
+    kv = kvals.split(",") if kname else [""]
+    runs = [(n, f, b, x) for n in args.shapes.split(",") for f in fv for b in bv for x in kv]
+    for shape, fvar, bvar, kval in runs:
         os.environ["SAE_FWD_VARIANT"], os.environ["SAE_BWD_VARIANT"] = fvar, bvar
+        if kname:
+            os.environ[kname] = kval
         name = shape + ("+rel" if args.rel else "") + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
+        name += f"@{kname}={kval}" if len(kv) > 1 else ""
         B, Nq, Nk, H, D = SHAPES[shape]
         g = torch.Generator(device=dev).manual_seed(0)
         q = torch.randn(B, Nq, H, D, device=dev, generator=g).to(dt)
