@@ -216,6 +216,27 @@ __device__ __forceinline__ bf16x8 th2_rowB(const char* img, int head, int s, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Head-dim tail on v_mfma_f32_16x16x32_bf16 (TAIL: D <= 48 at DP 64, rows d 32..47 of the query
+// pass's dQ^T product as two 16 x 16 blocks instead of half of a second 32 x 32 tile).  Operand k order:
+// standard, k = 8 (lane >> 4) + j.
+// A: image column col0 + (lane & 15) of a [row][DP] Img tile, k = image rows 8 (lane >> 4) + j
+template <int DP> __device__ __forceinline__ bf16x8 th2_colA16(const char* lds, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const int colb = col0 + 4 * (li & 3), chunk = colb >> 3, half = (colb >> 2) & 1;
+  const int r1 = 8 * g + (li >> 2), r2 = r1 + 4;
+  return th2_tr2(lds + r1 * (DP * 2) + 16 * (chunk ^ swz<DP>(r1)) + 8 * half,
+                 lds + r2 * (DP * 2) + 16 * (chunk ^ swz<DP>(r2)) + 8 * half);
+}
+// B of the query pass: image row `head` at position k * 32 + n, k = key, n = 16 bb + (lane & 15) (query)
+__device__ __forceinline__ bf16x8 th2_colB16(const char* img, int head, int bb, int lane) {
+  const int li = lane & 15, k1 = 8 * (lane >> 4) + (li >> 2);
+  const char* base = img + th2_ro(head) + (16 * bb + 4 * (li & 3)) * 2;
+  return th2_tr2(base + k1 * kTh2Blk, base + (k1 + 4) * kTh2Blk);
+}
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // sum of per-wave 16 x 16 partials (one per wave of the NW, in LDS scratch) -> this workgroup's dT
 // slot (the first 256 threads: NW >= 4 when H > 4)
 __device__ __forceinline__ void th2_dt_store(float* scratch, f32x4 acc, float* out, int H, int NW, int w, int lane,
@@ -517,7 +538,8 @@ template <int DP, int NWMAX, bool ROT = false, int HPW = 1, bool LEAN = false, i
 __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThArgs a) {
   static_assert(!LEAN || HPW == 1, "LEAN: one head per wave");
   using I = Img<__bf16, DP>;
-  constexpr int NS = NSU, NT = DP / 32;   // (NSU as in th2_fwd_kernel)
+  constexpr bool TAIL = DP == 64 && NSU == 3;   // dQ^T rows d 32..47 on 16 x 16 MFMAs (th2_colA16)
+  constexpr int NS = NSU, NT = TAIL ? 1 : DP / 32;   // (NSU as in th2_fwd_kernel)
   constexpr bool KST = NWMAX * HPW <= 8;
   constexpr int NR = KST ? 4 : 8;
   constexpr int IMG = th2_img<KST>();
@@ -721,10 +743,14 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThA
 
   // ---- pass B
   f32x16 adq[HPW][NT];
+  f32x4 adqt[HPW][2];   // TAIL: d 32..47, queries 16 bb + (lane & 15)
 #pragma unroll
-  for (int e = 0; e < HPW; ++e)
+  for (int e = 0; e < HPW; ++e) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) adq[e][t] = zero16();
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) adqt[e][bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   f32x4 dt1 = {0.f, 0.f, 0.f, 0.f};
   for (int kt = 0; kt < nkt; ++kt) {
     tiles(kt, true);   // (wave-private K images: after this wave's previous dQ reads)
@@ -769,6 +795,15 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThA
         for (int t = 0; t < NT; ++t)
           adq[e][t] = MF<__bf16>::mma(I::colfrag(ldsK[e], 0, s2, 32 * t, lane), sf, adq[e][t]);
       }
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int e = 0; e < HPW; ++e) {
+        const bf16x8 at = th2_colA16<DP>(ldsK[e], 32, lane);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+          adqt[e][bb] = mfma16(at, th2_colB16(XS, hv[e] ? hd[e] : w, bb, lane), adqt[e][bb]);
+      }
+    }
     __syncthreads();
   }
   // dT1 partial: XS held the SCALED scores (S = scale q k, the reference's logits)
@@ -792,6 +827,21 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThA
         }
     }
   }
+  if constexpr (TAIL) {   // query 16 bb + (lane & 15), d 32 + 4 (lane >> 4) .. + 3
+#pragma unroll
+    for (int e = 0; e < HPW; ++e) {
+      if (!hv[e]) continue;
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        const int qq = qb * 32 + 16 * bb + (lane & 15), d0 = 32 + 4 * (lane >> 4);
+        if (qq >= a.Nq) continue;
+        __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hd[e] * a.dqs[2] + (long long)qq * a.dqs[1];
+        const f32x4 x = adqt[e][bb];
+        store4<__bf16, true>(DQ, d0, a.D, (float)(__bf16)(x[0] * a.scale), (float)(__bf16)(x[1] * a.scale),
+                             (float)(__bf16)(x[2] * a.scale), (float)(__bf16)(x[3] * a.scale));
+      }
+    }
+  }
 }
 
 // =============================================================================== bwd: kv
@@ -802,6 +852,8 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThA
 // HPW = 2 (9..16 heads, eight waves of <= 256 registers): each wave keeps the dK / dV accumulators
 // of its two heads; the key block's K / V fragments are re-read per query tile (L2-resident, 4 KiB
 // per head) instead of held, and the dO / Q tiles go through one staging buffer per head.
+// (NSU 3 with the 16 x 16 head-dim tail, as in the query pass, measured level here: 230.4 vs
+// 229.9 us, 206 vs 226 VGPRs at the same occupancy -- profiles/r06u_th_tail_ab.txt)
 template <int DP, int NWMAX, bool ROT = false, int HPW = 1>
 __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
   using I = Img<__bf16, DP>;
@@ -999,6 +1051,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
         for (int t = 0; t < NT; ++t)
           adv[e][t] = MF<__bf16>::mma(I::colfrag(buf[e], 0, s2, 32 * t, lane), pf, adv[e][t]);
       }
+
       if constexpr (!TWO) {   // one buffer: Q after this wave's own dO reads
         if (rot) qst.rope(a.rope, qt * 32, lane);
         qst.write(bufQ[e], lane);
@@ -1010,6 +1063,7 @@ __global__ __launch_bounds__(64 * NWMAX) void th2_bwd_kv_kernel(ThArgs a) {
         for (int t = 0; t < NT; ++t)
           adk[e][t] = MF<__bf16>::mma(I::colfrag(bufQ[e], 0, s2, 32 * t, lane), sf, adk[e][t]);
       }
+
     }
     if constexpr (TWO) {
       if (qt + 1 < nqt) {   // wave-private images: after this wave's own reads

@@ -36,6 +36,7 @@ def _orth(rng, h):
     (2, 50, 50, 4, 48, "bf16"),      # cait_xxs heads
     (1, 45, 45, 9, 48, "bf16"),      # odd head count > 8: the last wave's second head is empty
     (1, 40, 33, 11, 32, "bf16"),     # 11 heads at head_dim 32, Nq != Nk
+    (1, 45, 37, 5, 40, "bf16"),      # D 40: the 16 x 16 head-dim tail (d 32..47) half past D, ragged blocks
 ])
 def test_talking_heads(dev, B, N, Nk, H, D, mode):
     import torch
