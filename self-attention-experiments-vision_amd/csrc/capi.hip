@@ -446,7 +446,8 @@ int th2_bwd_run(hipStream_t st, ThArgs a) {
 // CaiT-S24, 1.05x; profiles/r06s_th_lean_ab.txt)
 template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
   if constexpr (DP == 64)
-    if (a.H <= 8 && !a.rope.sin && a.D <= 48) return th2_fwd_run<64, 8, false, 1, true, 3>(st, a);
+    if (a.H <= 8 && a.D <= 48)
+      return a.rope.sin ? th2_fwd_run<64, 8, true, 1, true, 3>(st, a) : th2_fwd_run<64, 8, false, 1, true, 3>(st, a);
   if (a.rope.sin) return a.H <= 8 ? th2_fwd_run<DP, 8, true, 1, true>(st, a) : th2_fwd_run<DP, 8, true, 2>(st, a);
   return a.H <= 8 ? th2_fwd_run<DP, 8, false, 1, true>(st, a) : th2_fwd_run<DP, 8, false, 2>(st, a);
 }
@@ -454,8 +455,15 @@ template <int DP> int th2_fwd_dispatch(hipStream_t st, const ThArgs& a) {
 // backward 540 -> 474 us; profiles/r06s_th_lean_ab.txt)
 template <int DP> int th2_bwd_dispatch(hipStream_t st, const ThArgs& a) {
   if constexpr (DP == 64)
-    if (a.H <= 8 && !a.rope.sin && !dev_knob("SAE_TH_BWDQ_WIDE"))
-      return a.D <= 48 ? th2_bwd_run<64, 8, false, 1, true, 3>(st, a) : th2_bwd_run<64, 8, false, 1, true>(st, a);
+    if (a.H <= 8 && !dev_knob("SAE_TH_BWDQ_WIDE")) {
+      if (a.rope.sin) {
+        // (rotary at D <= 48: fwd + bwd 886 -> 785 us at CaiT-S24 shape; the query pass at one
+        // workgroup per CU, 210 VGPRs, 614 vs 572 us backward -- profiles/r06w_th_rotary_ab.txt)
+        if (a.D <= 48) return th2_bwd_run<64, 8, true, 1, true, 3>(st, a);
+      } else {
+        return a.D <= 48 ? th2_bwd_run<64, 8, false, 1, true, 3>(st, a) : th2_bwd_run<64, 8, false, 1, true>(st, a);
+      }
+    }
   if (a.rope.sin) return a.H <= 8 ? th2_bwd_run<DP, 8, true, 1>(st, a) : th2_bwd_run<DP, 8, true, 2>(st, a);
   return a.H <= 8 ? th2_bwd_run<DP, 8, false, 1>(st, a) : th2_bwd_run<DP, 8, false, 2>(st, a);
 }

@@ -836,9 +836,11 @@ __global__ __launch_bounds__(64 * NWMAX, LEAN ? 4 : 1) void th2_bwd_q_kernel(ThA
         const int qq = qb * 32 + 16 * bb + (lane & 15), d0 = 32 + 4 * (lane >> 4);
         if (qq >= a.Nq) continue;
         __bf16* DQ = reinterpret_cast<__bf16*>(a.dq) + b * a.dqs[0] + hd[e] * a.dqs[2] + (long long)qq * a.dqs[1];
-        const f32x4 x = adqt[e][bb];
-        store4<__bf16, true>(DQ, d0, a.D, (float)(__bf16)(x[0] * a.scale), (float)(__bf16)(x[1] * a.scale),
-                             (float)(__bf16)(x[2] * a.scale), (float)(__bf16)(x[3] * a.scale));
+        float x[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[c] = (float)(__bf16)(adqt[e][bb][c] * a.scale);
+        if (rot && d0 < a.D) rope_pairs<2, -1>(x, a.rope, qq, d0 / 2);
+        store4<__bf16, true>(DQ, d0, a.D, x[0], x[1], x[2], x[3]);
       }
     }
   }

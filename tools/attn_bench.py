@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
     ap.add_argument("--th", action="store_true", help="talking-heads attention (orthogonal T1, T2)")
+    ap.add_argument("--rope", action="store_true", help="fused rotary (base 10000) on q / k (--th)")
     ap.add_argument("--rel", action="store_true",
                     help="BoTNet relative logits (square Hs = Ws = sqrt(Nk) grid, N(0, 1/D) bias tables)")
     ap.add_argument("--fwd-variants", default="", help="comma list of SAE_FWD_VARIANT values to A/B (dev build: SAE_ATTN_LIB=<pkg>/libsae_attn_dev.so)")
@@ -62,7 +63,7 @@ def main():
         os.environ["SAE_FWD_VARIANT"], os.environ["SAE_BWD_VARIANT"] = fvar, bvar
         if kname:
             os.environ[kname] = kval
-        name = shape + ("+rel" if args.rel else "") + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
+        name = shape + ("+rel" if args.rel else "") + ("+rope" if args.rope else "") + (f"@f{fvar}" if len(fv) > 1 else "") + (f"@b{bvar}" if len(bv) > 1 else "")
         name += f"@{kname}={kval}" if len(kv) > 1 else ""
         B, Nq, Nk, H, D = SHAPES[shape]
         g = torch.Generator(device=dev).manual_seed(0)
@@ -74,9 +75,10 @@ def main():
         sc = 1.0 / math.sqrt(D)
         if args.th:
             th1, th2 = (torch.linalg.qr(torch.randn(H, H, device=dev, generator=g))[0].contiguous() for _ in range(2))
-            o, lse, _, _ = ops._th_fwd(q, k, v, th1, th2, sc)
-            fwd_call = lambda: ops._th_fwd(q, k, v, th1, th2, sc)
-            bwd_call = lambda: ops._th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, sc)
+            rp = 10000.0 if args.rope else None
+            o, lse, _, _ = ops._th_fwd(q, k, v, th1, th2, sc, rope=rp)
+            fwd_call = lambda: ops._th_fwd(q, k, v, th1, th2, sc, rope=rp)
+            bwd_call = lambda: ops._th_bwd(q, k, v, th1, th2, lse, do, dq, dk, dv, sc, rope=rp)
         elif args.rel:
             hs = int(round(math.sqrt(Nk)))
             assert hs * hs == Nk and Nq == Nk, "--rel: square key grid"
