@@ -169,6 +169,34 @@ def test_softmax_spike(dev, mode, gain):
         assert rel_err(t.grad, g[n]) <= TOL[mode], n
 
 
+@pytest.mark.parametrize("gain", [0.05, 0.6, 4.0, 8.0])
+def test_lone_key_spike(dev, gain):
+    """Nk = 64 n + 1 (ViT at 384 px: 576 patches + the class token): the last key tile holds one key
+    (half a tile of MFMA work, the rest masked).  A spike AT that key raises the row max in the last
+    tile (rescale / fixed-max fallback); an anti-spike keeps it far below."""
+    import torch
+    import sae_vision_amd.ops as ops
+
+    rng = np.random.default_rng(9)
+    B, N, H, D = 1, 321, 2, 64
+    q = randn(rng, (B, N, H, D), "bf16")
+    k = randn(rng, (B, N, H, D), "bf16") * 0.3
+    v = randn(rng, (B, N, H, D), "bf16")
+    k[0, N - 1, 0] = q[0, 5, 0] * gain                # the lone key: spike for query 5 of head 0
+    k[0, N - 1, 1] = -q[0, 200, 1] * gain             # and an anti-spike for query 200 of head 1
+    k = R.round_bf16(k)
+    tq, tk, tv = (torch.tensor(x, device=dev, dtype=torch.bfloat16, requires_grad=True) for x in (q, k, v))
+    o = ops.attention(tq, tk, tv)
+    do = randn(np.random.default_rng(2), (B, N, H, D), "bf16")
+    o.backward(torch.tensor(do, device=dev, dtype=torch.bfloat16))
+    o64 = R.attention_core_fwd(q, k, v, "f64")
+    assert rel_err(o, R.attention_core_fwd(q, k, v, "bf16", round_scores=False)) <= TOL["bf16"]
+    assert rel_err(o, o64) <= max(TOL["bf16"], rel_err(R.attention_core_fwd(q, k, v, "bf16"), o64))
+    g = R.attention_core_bwd(q, k, v, do)
+    for n, t in (("dq", tq), ("dk", tk), ("dv", tv)):
+        assert rel_err(t.grad, g[n]) <= TOL["bf16"], n
+
+
 @pytest.mark.parametrize("spike", [6, 12])
 def test_fixed_max_fallback(dev, spike):
     """The bf16 forward keeps the running max where the first key tile put it and redoes a block
