@@ -650,6 +650,10 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
   const long long tiles = (long long)((g0.M + BM - 1) / BM) * ((g0.N + BN - 1) / BN);
   const long long grid = std::min<long long>(tiles, device_cus());
   NtArgs g = g0;
+  // epilogue stores non-temporal except for the gelu' multiply (whose 96-byte row segments then
+  // left L2 unmerged: 77 -> 102 MB written); DeiT-S step 8.02 -> 7.96 ms with every epilogue
+  // non-temporal, the plain / GELU launches faster and the multiply slower (profiles/r06z_g8_nts_ab.txt)
+  g.nts = EPI != kEpiDGelu && !dev_knob("SAE_G8_NO_NTS");
 #ifdef SAE_DEV_KNOBS
   g.ctr = (NS == 2 && tiles > grid && grid >= 8 && dev_knob("SAE_G8_DYN")) ? g8_slot(st) : nullptr;
   if (g.ctr) {

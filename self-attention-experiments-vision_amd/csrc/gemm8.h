@@ -371,12 +371,15 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
         if (MODE == 1) {
           if (raw.x == 0x7fc07fc0u && raw.y == 0x12345678u) a.c[0] = (__bf16)1.f;   // keep the reads
         } else if (m < a.M && n < a.N) {
-          if constexpr (EPI == kEpiNone) {
-            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = raw;
-          } else if constexpr (EPI == kEpiGelu) {
-            gelu_store8(raw, a.gp, a.c + (long long)m * a.ldc + n, a.c2 + (long long)m * a.ldc + n);
+          __bf16* const cp = a.c + (long long)m * a.ldc + n;
+          if (a.nts) {   // (wave-uniform)
+            if constexpr (EPI == kEpiNone) st16<true>(cp, raw);
+            else if constexpr (EPI == kEpiGelu) gelu_store8<true>(raw, a.gp, cp, a.c2 + (long long)m * a.ldc + n);
+            else st16<true>(cp, dgelu8(raw, hv[ip][it], a.gp));
           } else {
-            *reinterpret_cast<uint4*>(a.c + (long long)m * a.ldc + n) = dgelu8(raw, hv[ip][it], a.gp);
+            if constexpr (EPI == kEpiNone) st16(cp, raw);
+            else if constexpr (EPI == kEpiGelu) gelu_store8(raw, a.gp, cp, a.c2 + (long long)m * a.ldc + n);
+            else st16(cp, dgelu8(raw, hv[ip][it], a.gp));
           }
         }
       }

@@ -45,6 +45,7 @@ struct NtArgs {
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
   int gp;              // kEpiGelu: c2 = gelu'(h) instead of h; kEpiDGelu: aux holds gelu'(h)
   unsigned* ctr;       // gemm8 dynamic tile walk: {ticket, done} counters of this launch's slot
+  int nts;             // gemm8: epilogue stores non-temporal (streamed past L2's normal allocation)
 };
 
 constexpr int kNtT = 128;   // output tile edge
@@ -106,7 +107,14 @@ __device__ __forceinline__ unsigned gelu_grad_bf2(unsigned hw, unsigned& gw) {
 __device__ __forceinline__ unsigned mul_bf2(unsigned dw, unsigned gw) {   // d * g (the gp backward epilogue)
   return f2_to_bf2(bf2_to_f2(dw) * bf2_to_f2(gw));
 }
+// a 16-byte output store; NT: non-temporal (the output stream does not displace the operands in L2)
+template <bool NT = false> __device__ __forceinline__ void st16(__bf16* p, const uint4& v) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  if constexpr (NT) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<uint4*>(p) = v;
+}
 // the GELU / GELU' epilogue stores of one 16-byte row segment (8 outputs)
+template <bool NT = false>
 __device__ __forceinline__ void gelu_store8(const uint4& raw, bool gp, __bf16* c, __bf16* c2) {
   if (gp) {
     uint4 g, y;
@@ -114,11 +122,11 @@ __device__ __forceinline__ void gelu_store8(const uint4& raw, bool gp, __bf16* c
     y.y = gelu_grad_bf2(raw.y, g.y);
     y.z = gelu_grad_bf2(raw.z, g.z);
     y.w = gelu_grad_bf2(raw.w, g.w);
-    *reinterpret_cast<uint4*>(c2) = g;
-    *reinterpret_cast<uint4*>(c) = y;
+    st16<NT>(c2, g);
+    st16<NT>(c, y);
   } else {
-    *reinterpret_cast<uint4*>(c2) = raw;
-    *reinterpret_cast<uint4*>(c) = uint4{gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)};
+    st16<NT>(c2, raw);
+    st16<NT>(c, uint4{gelu_bf2(raw.x), gelu_bf2(raw.y), gelu_bf2(raw.z), gelu_bf2(raw.w)});
   }
 }
 __device__ __forceinline__ uint4 dgelu8(const uint4& raw, const uint4& hv, bool gp) {
