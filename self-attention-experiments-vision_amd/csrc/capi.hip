@@ -652,8 +652,10 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
   NtArgs g = g0;
   // epilogue stores non-temporal except for the gelu' multiply (whose 96-byte row segments then
   // left L2 unmerged: 77 -> 102 MB written); DeiT-S step 8.02 -> 7.96 ms with every epilogue
-  // non-temporal, the plain / GELU launches faster and the multiply slower (profiles/r06z_g8_nts_ab.txt)
-  g.nts = EPI != kEpiDGelu && !dev_knob("SAE_G8_NO_NTS");
+  // non-temporal, the plain / GELU launches faster and the multiply slower (profiles/r06z_g8_nts_ab.txt).
+  // The multiply's aux (gelu'(h)) tile loaded non-temporal: level in isolation, DeiT-S step
+  // 8.01 -> 7.85 ms (profiles/r06z4_g8_aux_nt_ab.txt)
+  g.nts = (EPI != kEpiDGelu && !dev_knob("SAE_G8_NO_NTS") ? 1 : 0) | (!dev_knob("SAE_G8_NO_AUX_NT") ? 2 : 0);
 #ifdef SAE_DEV_KNOBS
   g.ctr = (NS == 2 && tiles > grid && grid >= 8 && dev_knob("SAE_G8_DYN")) ? g8_slot(st) : nullptr;
   if (g.ctr) {

@@ -307,9 +307,15 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
             const int id = it * 64 + lane;
             const int rr = id / SCH, c = id % SCH;
             const int m = m0 + 32 * ip + rr, n = nw + 8 * c;
-            hv[ip][it] = (32 * ip + rr < C::WM && m < a.M && n < a.N)
-                             ? *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n)
-                             : uint4{0u, 0u, 0u, 0u};
+            const bool in = 32 * ip + rr < C::WM && m < a.M && n < a.N;
+            if (a.nts & 2) {   // aux streamed (non-temporal load): read once, not kept in L2
+              typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+              const u32x4 v = in ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.aux + (long long)m * a.ldaux + n))
+                                 : u32x4{0u, 0u, 0u, 0u};
+              hv[ip][it] = uint4{v[0], v[1], v[2], v[3]};
+            } else {
+              hv[ip][it] = in ? *reinterpret_cast<const uint4*>(a.aux + (long long)m * a.ldaux + n) : uint4{0u, 0u, 0u, 0u};
+            }
           }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
           if (raw.x == 0x7fc07fc0u && raw.y == 0x12345678u) a.c[0] = (__bf16)1.f;   // keep the reads
         } else if (m < a.M && n < a.N) {
           __bf16* const cp = a.c + (long long)m * a.ldc + n;
-          if (a.nts) {   // (wave-uniform)
+          if (a.nts & 1) {   // (wave-uniform)
             if constexpr (EPI == kEpiNone) st16<true>(cp, raw);
             else if constexpr (EPI == kEpiGelu) gelu_store8<true>(raw, a.gp, cp, a.c2 + (long long)m * a.ldc + n);
             else st16<true>(cp, dgelu8(raw, hv[ip][it], a.gp));

@@ -45,7 +45,8 @@ struct NtArgs {
   PatchGeom pg;        // patch-embedding A operand (patch.h), unused otherwise
   int gp;              // kEpiGelu: c2 = gelu'(h) instead of h; kEpiDGelu: aux holds gelu'(h)
   unsigned* ctr;       // gemm8 dynamic tile walk: {ticket, done} counters of this launch's slot
-  int nts;             // gemm8: epilogue stores non-temporal (streamed past L2's normal allocation)
+  int nts;             // gemm8: 1 = epilogue stores non-temporal (streamed past L2's normal
+                       // allocation), 2 = the gelu' aux tile loaded non-temporal
 };
 
 constexpr int kNtT = 128;   // output tile edge
