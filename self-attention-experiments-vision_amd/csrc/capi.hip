@@ -644,9 +644,9 @@ static unsigned* g8_slot(hipStream_t st) {
 // one persistent gemm8 launch (BM x BN tiles, one 8-wave workgroup per CU).  The work-stealing walk
 // (DYN, dev builds: SAE_G8_DYN=1) measured 3 % slower on the DeiT-S step and no better under the
 // one-GPU RCCL contention emulation (profiles/r06c_g8_dyn_ab.txt), so the release walk is static.
-template <int EPI, int BN, int BK, int NS, int BM>
+template <int EPI, int BN, int BK, int NS, int BM, int WGM = 2>
 static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
-  constexpr int lds = g8_lds_bytes<BN, BK, NS>() + kG8TickBytes;
+  constexpr int lds = g8_lds_bytes<BN, BK, NS, WGM>() + kG8TickBytes;
   const long long tiles = (long long)((g0.M + BM - 1) / BM) * ((g0.N + BN - 1) / BN);
   const long long grid = std::min<long long>(tiles, device_cus());
   NtArgs g = g0;
@@ -666,8 +666,8 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
     }
   }
 #endif
-  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>, lds)) return rc;
-  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM>, lds)) return rc;
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM>), dim3((unsigned)grid), dim3(512), lds, st, g);
   return 0;
 }
 template <int EPI, int BN, int BK, int NS>
@@ -1462,7 +1462,10 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
 #endif
   ) {
     if (epilogue == SAE_EPI_GELU && g8_gelu_bn128(M, N, K)) {
-      if (int rc = g8_launch_bm<kEpiGelu, 128, 64, 2, 256>(g, st)) return rc;
+      // 4 x 2 waves (64 x 64 wave tiles): whole 128-byte output lines per wave row segment --
+      // writes 172 -> 155 MB (= algorithmic), 57.1 -> 54.8 us at DeiT-S (profiles/r06w4_g8_wgm4_ab.txt)
+      if (int rc = dev_knob("SAE_G8_WGM2") ? g8_launch_bm<kEpiGelu, 128, 64, 2, 256>(g, st)
+                                           : g8_launch_bm<kEpiGelu, 128, 64, 2, 256, 4>(g, st)) return rc;
       return check_launch("gemm8_nt");
     }
     const int rc = epilogue == SAE_EPI_NONE   ? g8_launch<kEpiNone, 192, 64, 2>(g, st)

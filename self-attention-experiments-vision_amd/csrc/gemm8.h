@@ -85,17 +85,19 @@ template <int BK> __device__ __forceinline__ int g8_swz(int r) {
 // BM: tile rows (256, or 224 where 256-row tiles leave CUs idle: M = 25,216 into 384 features is
 // 198 tiles of 256 x 192 on 256 CUs but 226 of 224 x 192; the A image keeps 256 rows, the rows past
 // BM read as zero through the descriptor's range check -- no memory traffic)
-template <int BN, int BM = 256> struct G8Cfg {
+// WGM: waves along M (2: 2 x 4 waves; 4: 4 x 2 -- 64 x 64 wave tiles at 256 x 128, so each wave's
+// epilogue row segment is a whole 128-byte line)
+template <int BN, int BM = 256, int WGM = 2> struct G8Cfg {
   static_assert(BM % 32 == 0 && BM <= 256, "tile rows");
-  static constexpr int WM = BM / 2, WN = BN / 4;  // wave tile (2 x 4 waves)
+  static constexpr int WM = BM / WGM, WN = BN / (8 / WGM);  // wave tile
   static constexpr int MT = WM / 16, NT = WN / 16; // 16 x 16 accumulator tiles per wave
 };
 
 // LDS: the stage ring, then one 32-row epilogue scratch per wave (rows padded by 16 bytes)
 template <int BN, int BK, int NS> constexpr int g8_ring_bytes() { return NS * (256 + BN) * BK * 2; }
-template <int BN> constexpr int g8_scratch_bytes() { return 32 * (BN / 4 * 2 + 16); }
-template <int BN, int BK, int NS> constexpr int g8_lds_bytes() {
-  return g8_ring_bytes<BN, BK, NS>() + 8 * g8_scratch_bytes<BN>();
+template <int BN, int WGM = 2> constexpr int g8_scratch_bytes() { return 32 * (BN / (8 / WGM) * 2 + 16); }
+template <int BN, int BK, int NS, int WGM = 2> constexpr int g8_lds_bytes() {
+  return g8_ring_bytes<BN, BK, NS>() + 8 * g8_scratch_bytes<BN, WGM>();
 }
 constexpr int kG8TickBytes = 16;   // the DYN ticket word after the scratch images
 
@@ -121,11 +123,11 @@ constexpr int kG8TickBytes = 16;   // the DYN ticket word after the scratch imag
 // it: results are bit-identical to the static walk (tools/g8_dyn_check.py).  Placement only decides
 // speed: every group has workgroups (G >= 8), and each drains its own counter.
 // MODE (probe builds only): 0 = the kernel; 1 = no global stores; 2 = no MFMAs (staging only)
-template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256, bool DYN = false>
+template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256, bool DYN = false, int WGM = 2>
 __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   static_assert(!DYN || NS == 2, "dynamic walk: the ticket atomic rides on the vmcnt(0) stage waits of NS = 2");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using C = G8Cfg<BN, BM>;
+  using C = G8Cfg<BN, BM, WGM>;
   constexpr int RB = BK * 2;                  // image row bytes
   constexpr int CPR = BK / 8;                 // 16-byte chunks per row
   constexpr int RPP = 64 / CPR;               // rows per 1-KiB piece
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   const int myt = DYN ? 0x3fffffff : (ntiles - b0 + G - 1) / G;
   const int nst = a.K / BK;
   int total = DYN ? 0x7fffffff : myt * nst;   // stages of this workgroup's stream (DYN: found at the end)
-  volatile unsigned* tick = reinterpret_cast<volatile unsigned*>(smem + g8_lds_bytes<BN, BK, NS>());
+  volatile unsigned* tick = reinterpret_cast<volatile unsigned*>(smem + g8_lds_bytes<BN, BK, NS, WGM>());
   unsigned tkv = 0;                           // wave 0: the returning ticket atomic in flight
   int tile_e = b0, tile_o = b0;               // DYN: tile ids of the even / odd local tiles
   auto tile_of = [&](int it) { return __builtin_amdgcn_readfirstlane((it & 1) ? tile_o : tile_e); };
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 2, wc = w & 3;
+  const int wr = w / (8 / WGM), wc = w % (8 / WGM);
   const unsigned lbase = __builtin_amdgcn_readfirstlane(
       (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
 
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
   constexpr int SRB = C::WN * 2 + 16;             // scratch row bytes (wave tile row + pad)
   constexpr int SCH = C::WN / 8;                  // 16-byte chunks per tile row
   uint4 hv[EPI == kEpiDGelu ? (C::MT + 1) / 2 : 1][EPI == kEpiDGelu ? 32 * SCH / 64 : 1];   // GELU' aux tile
-  char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN>();
+  char* scratch = smem + g8_ring_bytes<BN, BK, NS>() + w * g8_scratch_bytes<BN, WGM>();
 
   if constexpr (DYN) {
     // the first tile: drawn, published through LDS, then the second tile's ticket goes out
