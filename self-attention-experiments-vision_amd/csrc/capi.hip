@@ -650,12 +650,12 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
   const long long tiles = (long long)((g0.M + BM - 1) / BM) * ((g0.N + BN - 1) / BN);
   const long long grid = std::min<long long>(tiles, device_cus());
   NtArgs g = g0;
-  // epilogue stores non-temporal except for the gelu' multiply (whose 96-byte row segments then
+  // epilogue stores non-temporal except for the gelu' multiply on 2 x 4 waves (whose 96-byte row segments then
   // left L2 unmerged: 77 -> 102 MB written); DeiT-S step 8.02 -> 7.96 ms with every epilogue
   // non-temporal, the plain / GELU launches faster and the multiply slower (profiles/r06z_g8_nts_ab.txt).
   // The multiply's aux (gelu'(h)) tile loaded non-temporal: level in isolation, DeiT-S step
   // 8.01 -> 7.85 ms (profiles/r06z4_g8_aux_nt_ab.txt)
-  g.nts = (EPI != kEpiDGelu && !dev_knob("SAE_G8_NO_NTS") ? 1 : 0) | (!dev_knob("SAE_G8_NO_AUX_NT") ? 2 : 0);
+  g.nts = ((EPI != kEpiDGelu || WGM == 4) && !dev_knob("SAE_G8_NO_NTS") ? 1 : 0) | (!dev_knob("SAE_G8_NO_AUX_NT") ? 2 : 0);
 #ifdef SAE_DEV_KNOBS
   g.ctr = (NS == 2 && tiles > grid && grid >= 8 && dev_knob("SAE_G8_DYN")) ? g8_slot(st) : nullptr;
   if (g.ctr) {
@@ -1466,6 +1466,12 @@ int sae_gemm_nt(void* stream, int32_t M, int32_t N, int32_t K, const void* a, in
       // writes 172 -> 155 MB (= algorithmic), 57.1 -> 54.8 us at DeiT-S (profiles/r06w4_g8_wgm4_ab.txt)
       if (int rc = dev_knob("SAE_G8_WGM2") ? g8_launch_bm<kEpiGelu, 128, 64, 2, 256>(g, st)
                                            : g8_launch_bm<kEpiGelu, 128, 64, 2, 256, 4>(g, st)) return rc;
+      return check_launch("gemm8_nt");
+    }
+    // the gelu' multiply on the same 256 x 128 tiles and 4 x 2 waves (whole-line stores, now also
+    // non-temporal): 59.5 -> 53.8 us at DeiT-S, reads 128 -> 111 MB (profiles/r06m128_g8_mul_ab.txt)
+    if (epilogue == SAE_EPI_DGELU && !dev_knob("SAE_G8_MUL192") && g8_gelu_bn128(M, N, K)) {
+      if (int rc = g8_launch_bm<kEpiDGelu, 128, 64, 2, 256, 4>(g, st)) return rc;
       return check_launch("gemm8_nt");
     }
     const int rc = epilogue == SAE_EPI_NONE   ? g8_launch<kEpiNone, 192, 64, 2>(g, st)
