@@ -644,7 +644,7 @@ static unsigned* g8_slot(hipStream_t st) {
 // one persistent gemm8 launch (BM x BN tiles, one 8-wave workgroup per CU).  The work-stealing walk
 // (DYN, dev builds: SAE_G8_DYN=1) measured 3 % slower on the DeiT-S step and no better under the
 // one-GPU RCCL contention emulation (profiles/r06c_g8_dyn_ab.txt), so the release walk is static.
-template <int EPI, int BN, int BK, int NS, int BM, int WGM = 2>
+template <int EPI, int BN, int BK, int NS, int BM, int WGM = 2, bool XW = false>
 static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
   constexpr int lds = g8_lds_bytes<BN, BK, NS, WGM>() + kG8TickBytes;
   const long long tiles = (long long)((g0.M + BM - 1) / BM) * ((g0.N + BN - 1) / BN);
@@ -666,8 +666,8 @@ static int g8_launch_bm(const NtArgs& g0, hipStream_t st) {
     }
   }
 #endif
-  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM>, lds)) return rc;
-  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM>), dim3((unsigned)grid), dim3(512), lds, st, g);
+  if (int rc = lds_attr((const void*)gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM, XW>, lds)) return rc;
+  hipLaunchKernelGGL((gemm8_nt_kernel<EPI, BN, BK, NS, 0, BM, false, WGM, XW>), dim3((unsigned)grid), dim3(512), lds, st, g);
   return 0;
 }
 template <int EPI, int BN, int BK, int NS>
@@ -679,6 +679,12 @@ static int g8_launch(const NtArgs& g, hipStream_t st) {
                                              : g8_launch_bm<EPI, BN, 32, 4, 256>(g, st);
   }
 #endif
+  // plain 192-wide tiles: whole-row epilogue stores through the shared row image (XW): QKV forward
+  // 32.9 -> 31.4 us, DeiT-S step -0.13 % (profiles/r06xw_g8_xw_ab.txt)
+  if constexpr (EPI == kEpiNone && BN == 192)
+    if (!dev_knob("SAE_G8_NO_XW"))
+      return g8_pick_bm(g.M, g.N, BN) == 224 ? g8_launch_bm<EPI, BN, BK, NS, 224, 2, true>(g, st)
+                                             : g8_launch_bm<EPI, BN, BK, NS, 256, 2, true>(g, st);
   return g8_pick_bm(g.M, g.N, BN) == 224 ? g8_launch_bm<EPI, BN, BK, NS, 224>(g, st)
                                          : g8_launch_bm<EPI, BN, BK, NS, 256>(g, st);
 }

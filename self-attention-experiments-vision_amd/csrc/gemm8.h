@@ -123,8 +123,13 @@ constexpr int kG8TickBytes = 16;   // the DYN ticket word after the scratch imag
 // it: results are bit-identical to the static walk (tools/g8_dyn_check.py).  Placement only decides
 // speed: every group has workgroups (G >= 8), and each drains its own counter.
 // MODE (probe builds only): 0 = the kernel; 1 = no global stores; 2 = no MFMAs (staging only)
-template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256, bool DYN = false, int WGM = 2>
+// XW (plain epilogue, 2 x 4 waves): the four waves of a wave row stage their 32-row pieces into one
+// shared [32][BN] image and store whole rows (BN = 192: three full 128-byte lines per row instead of
+// four 96-byte pieces), two workgroup barriers per 32-row group
+template <int EPI, int BN, int BK, int NS, int MODE = 0, int BM = 256, bool DYN = false, int WGM = 2, bool XW = false>
 __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
+  static_assert(!XW || (EPI == kEpiNone && WGM == 2 && 64 * (BN * 2 + 16) <= 8 * g8_scratch_bytes<BN, WGM>()),
+                "XW: plain epilogue, 2 x 4 waves, the two row images fit the scratch");
   static_assert(!DYN || NS == 2, "dynamic walk: the ticket atomic rides on the vmcnt(0) stage waits of NS = 2");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using C = G8Cfg<BN, BM, WGM>;
@@ -353,6 +358,41 @@ __global__ __launch_bounds__(512, 1) void gemm8_nt_kernel(NtArgs a) {
       const int n = nw + 16 * j + 4 * fg;
       bv[j] = (EPI != kEpiDGelu && a.bias && n < a.N) ? *reinterpret_cast<const f32x4*>(a.bias + n)
                                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (XW) {
+      constexpr int XRB = BN * 2 + 16, XCH = BN / 8;   // row image bytes, 16-byte chunks per row
+      char* const xs = smem + g8_ring_bytes<BN, BK, NS>() + wr * 32 * XRB;
+      const int mrow = (t / tn) * BM + C::WM * wr, ncol = (t % tn) * BN;
+#pragma unroll
+      for (int ip = 0; ip < (C::MT + 1) / 2; ++ip) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int i = 2 * ip + h2;
+          if (i >= C::MT) break;
+#pragma unroll
+          for (int j = 0; j < C::NT; ++j) {
+            const bf16x4 v = {(__bf16)(acc[i][j][0] + bv[j][0]), (__bf16)(acc[i][j][1] + bv[j][1]),
+                              (__bf16)(acc[i][j][2] + bv[j][2]), (__bf16)(acc[i][j][3] + bv[j][3])};
+            *reinterpret_cast<bf16x4*>(xs + (16 * h2 + fr) * XRB + 2 * (C::WN * wc + 16 * j + 4 * fg)) = v;
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 32 * XCH / 256; ++it) {
+          const int id = (4 * it + wc) * 64 + lane;
+          const int rr = id / XCH, c = id % XCH;
+          const uint4 raw = *reinterpret_cast<const uint4*>(xs + rr * XRB + 16 * c);
+          const int m = mrow + 32 * ip + rr, n = ncol + 8 * c;
+          if (32 * ip + rr < C::WM && m < a.M && n < a.N) {
+            __bf16* const cp = a.c + (long long)m * a.ldc + n;
+            if (a.nts & 1) st16<true>(cp, raw);
+            else st16(cp, raw);
+          }
+        }
+        __syncthreads();
+      }
+      continue;
     }
 #pragma unroll
     for (int ip = 0; ip < (C::MT + 1) / 2; ++ip) {
